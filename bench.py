@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark: Poisson MLUPS + steps/sec of the lid-driven cavity projection
+solver (BASELINE.json metric), 4096^2 fp64 cells per GPU, weak-scaled row strips.
+
+A "step" is one full projection timestep of the reference algorithm
+(cavity-01.cpp:387-390): velocity BCs, predictor, source, SOR pressure solve to
+the reference tolerance (1e-9 * max|source|, capped at 10000 sweeps), corrector.
+All inputs are device-resident when the timed region starts.
+
+  value = interior cells x SOR iterations summed over all ranks / wall time of
+          the K timed steps (max over ranks), in MLUPS.
+
+Extra fields: steps_per_sec, roofline (fused red-black SOR kernel, HIP events on
+the solver's stream over the timed region), cpu_baseline (the oracle's
+lexicographic SOR loop — the reference's loop restated in C — on a bounded
+sample of the same grid, rank 0 only).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+For N > 1 launch with torch.distributed.run (one rank per GPU); halos and the
+residual all-reduce travel over RCCL inside libcfd_amd.so.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "computational-fluid-dynamics_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_CELL = 24.0  # SOR launch: read p_in + read f + write p_out, fp64
+METRIC = "Poisson MLUPS + steps/sec, cavity 4096² @1/2/4/8 GPU; % HBM roofline"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(nx: int, ny: int, budget_s: float) -> dict:
+    """The reference's SOR loop (sweep + residual per iteration, cavity-01.cpp:635-678)
+    restated in C (oracle/), single core, on the same grid for a bounded time."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from cfd_amd.params import make_params
+
+    cp = make_params("cavity", nx=nx, ny=ny)
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.velocity_bc(False)
+    o.tentative()
+    o.source()
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        o.poisson_fixed(1)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 1000:
+            break
+    del o
+    mlups = nx * ny * n / el / 1e6
+    return {"value": round(mlups, 3), "unit": "MLUPS", "cores": 1, "kind": "port",
+            "sample": f"{n} lexicographic SOR sweeps + residual (reference loop restated in C, gcc -O2) on the "
+                      f"{nx}x{ny} cavity after one predictor step, {el:.1f} s single-threaded"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--nx", type=int, default=4096)
+    ap.add_argument("--ny", type=int, default=4096, help="rows per GPU (weak scaling)")
+    ap.add_argument("--re", type=float, default=1000.0)
+    ap.add_argument("--max-iters", type=int, default=10000)
+    ap.add_argument("--check-every", type=int, default=0, help="residual test cadence (0: 1 on 1 GPU, 8 on >1)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    n_gpus = world
+
+    import torch  # noqa: E402  (first: PyTorch's HIP runtime is the one the library binds to)
+    import torch.distributed as dist
+
+    import cfd_amd as C
+    from cfd_amd import _lib
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    check_every = args.check_every or (1 if world == 1 else 8)
+    cp = C.make_params("cavity", re=args.re, nx=args.nx, ny=args.ny * world, max_iters=args.max_iters)
+    comm = None
+    if world > 1:
+        import ctypes
+        buf = (ctypes.c_ubyte * _lib.COMM_ID_BYTES)()
+        if rank == 0:
+            _lib.check(_lib.lib().cfd_comm_unique_id(buf), "cfd_comm_unique_id")
+        obj = [bytes(buf)]
+        dist.broadcast_object_list(obj, src=0)
+        buf = (ctypes.c_ubyte * _lib.COMM_ID_BYTES).from_buffer_copy(obj[0])
+        comm = _lib.lib().cfd_comm_init(buf, world, rank, local_rank)
+        if not comm:
+            raise _lib.CfdError("cfd_comm_init: " + _lib.lib().cfd_last_error().decode())
+        rows = (rank * args.ny + 1, (rank + 1) * args.ny)
+        solver = C.CavitySolver(cp, device=local_rank, check_every=check_every, rank_rows=rows, comm=comm)
+    else:
+        solver = C.CavitySolver(cp, device=local_rank, check_every=check_every)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    solver.applyBoundaryConditions()
+    for _ in range(args.warmup):
+        solver.step()
+    solver.synchronize()
+    solver.reset_timing()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    iters = []
+    for _ in range(args.steps):
+        it, _res = solver.step()
+        iters.append(it)
+    solver.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    tm = solver.timing()
+
+    updates = float(tm.poisson_cell_updates)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        u = torch.tensor([updates], dtype=torch.float64)
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        updates = float(u.item())
+
+    if rank == 0:
+        g0, g1 = solver.owned_rows()
+        wrows = (g1 - g0 + 1) + (1 if g0 == 1 else 0) + (1 if g1 == cp.ny else 0)
+        cells_per_launch = wrows * (cp.nx + 2)
+        avg_launch_ms = tm.poisson_ms / max(tm.poisson_launches, 1)
+        achieved = BYTES_PER_CELL * cells_per_launch / (avg_launch_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "poisson_pmc.json")
+        if os.path.exists(pmc):
+            try:
+                d = json.load(open(pmc))
+                if d.get("nx") == cp.nx and d.get("rows") == wrows:
+                    traffic = d.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        mlups = updates / elapsed / 1e6
+        line = {
+            "metric": METRIC,
+            "value": round(mlups, 2),
+            "unit": "MLUPS",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"lid-driven cavity Re={args.re:g}, {cp.nx}x{args.ny} fp64 cells per GPU "
+                            f"(global {cp.nx}x{cp.ny}), reference SOR tolerance {cp.tol_factor:g}*max|src|, "
+                            f"cap {cp.max_iters} sweeps/step",
+                "nx": cp.nx, "ny_per_gpu": args.ny, "global_ny": cp.ny,
+                "parallelism": f"strip{n_gpus}", "check_every": check_every,
+            },
+            "steps_per_sec": round(args.steps / elapsed, 4),
+            "sor_iterations_per_step": iters,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "poisson_rbsor_kernel<cavity>",
+                "bytes_per_launch": BYTES_PER_CELL * cells_per_launch,
+                "avg_launch_us": round(avg_launch_ms * 1e3, 2),
+            },
+        }
+        if not args.no_cpu_baseline:
+            log("timing the CPU baseline ...")
+            line["cpu_baseline"] = cpu_baseline(cp.nx, args.ny, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+
+    solver.close()
+    if comm:
+        _lib.lib().cfd_comm_destroy(comm)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,617 @@
+// kernels.hpp — HIP kernels for the projection-method timestep on gfx950.
+//
+// Device-side restatement of the reference's per-timestep path
+// (cavity-01.cpp, channel-01.cpp, backwards_step-01.cpp); every kernel cites
+// the reference loop it replaces. Floating-point expressions keep the
+// reference's operand order and the library is built with -ffp-contract=off,
+// so the stencil kernels are bit-identical to the reference loops.
+//
+// Layout: each field of a strip is a row-major slab of
+// `nrows` x `pitch` doubles; global cell (j, i) lives at
+// (j - row_lo) * pitch + i. Row 0 / ny+1 and column 0 / nx+1 are the
+// reference's ghost layers; a strip additionally stores HALO rows of its
+// neighbours on each side.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cfd {
+
+constexpr int CAVITY = 0, CHANNEL = 1, BACKSTEP = 2;
+constexpr int HALO = 4;           // halo rows stored per side (Poisson needs 4)
+constexpr int RES_SHARDS = 32;    // residual / max accumulators, one 128-B line each
+constexpr int SHARD_STRIDE = 16;  // doubles between shards (128 B)
+constexpr int RING = 4;           // residual ring slots (iteration k uses k & 3)
+
+struct Geo {
+  int nx, ny;      // global interior cells
+  int pitch;       // doubles per stored row
+  int row_lo;      // global row index of stored row 0
+  int nrows;       // stored rows
+  int j0, j1;      // owned interior rows (global, inclusive)
+  int wj0, wj1;    // owned rows incl. physical ghost rows on boundary strips
+};
+
+struct Coef {
+  int case_id;
+  int step_i, inlet_jmax;  // backwards step: solid block is i <= step_i, j > inlet_jmax
+  double dx, dy;
+  double idx, idy, idx2, idy2;  // 1/dx, 1/dy, 1/(dx*dx), 1/(dy*dy)
+  double nu, dt, rho, u_ref;
+  double omega;
+  double h2;               // cavity: grid_spacing * grid_spacing
+  double denom;            // open cases: 2*(idx2+idy2)
+  double cav_src;          // cavity: (1/dt) * rho           (cavity-01.cpp:624)
+  double open_src;         // open:   rho / dt               (channel-01.cpp:610)
+  double cav_corr;         // cavity: (dt/h) * rho           (cavity-01.cpp:696,701)
+  double open_cu, open_cv; // open:   dt/(rho*dx), dt/(rho*dy) (channel-01.cpp:697,701)
+  double tol_factor, abs_tol;
+};
+
+// Control block for one Poisson solve (device memory).
+struct PoissonCtl {
+  double* ring;        // RING x RES_SHARDS x SHARD_STRIDE residual accumulators
+  const double* tol;   // [0] tolerance, [1] initial residual (set by tol_kernel)
+  int* stop;           // [0] converged flag, [1] iteration count at convergence
+  int check_every;
+};
+
+__device__ __forceinline__ size_t at(const Geo& g, int j, int i) {
+  return (size_t)(j - g.row_lo) * (size_t)g.pitch + (size_t)i;
+}
+
+// backwards_step-01.cpp:492-520 (analytic mask: solid block upstream of the
+// step above the inlet channel); cavity / channel: every interior cell fluid.
+__device__ __forceinline__ bool is_fluid(const Coef& c, int nx, int ny, int j, int i) {
+  if (i < 1 || i > nx || j < 1 || j > ny) return false;
+  if (c.case_id != BACKSTEP) return true;
+  return (i > c.step_i) || (j <= c.inlet_jmax);
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Block-wide max of non-negative values -> one atomicMax on a shard.
+template <int NT>
+__device__ __forceinline__ void block_max_to_shard(double v, double* shards, int shard) {
+  __shared__ double red[NT / 64];
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = red[0];
+#pragma unroll
+    for (int k = 1; k < NT / 64; ++k) m = fmax(m, red[k]);
+    // Non-negative doubles order like their bit patterns.
+    atomicMax(reinterpret_cast<unsigned long long*>(shards + (size_t)shard * SHARD_STRIDE),
+              (unsigned long long)__double_as_longlong(m));
+  }
+}
+
+// Deterministic block sum (fixed butterfly + fixed wave order).
+template <int NT>
+__device__ __forceinline__ double block_sum(double v) {
+  __shared__ double red[NT / 64];
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) {
+    s = red[0];
+#pragma unroll
+    for (int k = 1; k < NT / 64; ++k) s += red[k];
+  }
+  return s;  // valid in thread 0
+}
+
+// ------------------------------------------------------------------ BCs --
+
+// cavity-01.cpp:523-543: moving lid + no-slip walls by ghost reflection.
+__global__ void bc_cavity_kernel(Geo g, Coef c, double* __restrict__ u, double* __restrict__ v) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nx = g.nx, ny = g.ny;
+  if (t <= nx) {
+    if (g.wj1 == ny + 1) u[at(g, ny + 1, t)] = 2.0 * c.u_ref - u[at(g, ny, t)];
+    if (g.wj0 == 0) u[at(g, 0, t)] = -u[at(g, 1, t)];
+  }
+  const int vj_lo = g.wj0, vj_hi = g.wj1 < ny ? g.wj1 : ny;
+  const int j = vj_lo + t;
+  if (j <= vj_hi) {
+    v[at(g, j, nx + 1)] = -v[at(g, j, nx)];
+    v[at(g, j, 0)] = -v[at(g, j, 1)];
+  }
+}
+
+// channel-01.cpp:513-529 / backwards_step-01.cpp:616-653, phases a-h merged:
+// every write is computed from the pre-call state plus the in-call writes it
+// depends on in the reference's order (u[1][0], u[ny][0], u[1][nx], u[ny][nx]).
+__global__ void bc_open_kernel(Geo g, Coef c, double* __restrict__ u, double* __restrict__ v) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nx = g.nx, ny = g.ny;
+  const int jin = (c.case_id == BACKSTEP) ? c.inlet_jmax : ny;
+  // column phases on owned rows: (a) u inlet, (b) v inlet, (c) u outlet, (d) v outlet
+  const int j = g.wj0 + t;
+  if (j <= g.wj1) {
+    if (j >= 1 && j <= ny) {
+      u[at(g, j, 0)] = (j <= jin) ? c.u_ref : 0.0;
+      u[at(g, j, nx)] = u[at(g, j, nx - 1)];
+    }
+    if (j >= 0 && j <= ny) {
+      v[at(g, j, 0)] = 0.0;
+      // (d) on the boundary rows is done by the row phase's i == nx thread, which
+      // must read v[j][nx] before (e)/(g) zero it (the reference order)
+      const bool zrow = (j == 0 && g.wj0 == 0) || (j == ny && g.wj1 == ny + 1);
+      if (!zrow) v[at(g, j, nx + 1)] = v[at(g, j, nx)];
+    }
+  }
+  // row phases (e)-(h) on the physical boundary rows
+  if (t <= nx) {
+    const int i = t;
+    if (g.wj0 == 0) {
+      if (i == nx) v[at(g, 0, nx + 1)] = v[at(g, 0, nx)];
+      if (i >= 1) v[at(g, 0, i)] = 0.0;
+      // (f) u[0][i] = -u[1][i], with u[1][0] / u[1][nx] as set by (a) / (c)
+      double u1;
+      if (i == 0) u1 = (1 <= jin) ? c.u_ref : 0.0;
+      else if (i == nx) u1 = u[at(g, 1, nx - 1)];
+      else u1 = u[at(g, 1, i)];
+      u[at(g, 0, i)] = -u1;
+    }
+    if (g.wj1 == ny + 1) {
+      if (i == nx) v[at(g, ny, nx + 1)] = v[at(g, ny, nx)];
+      if (i >= 1) v[at(g, ny, i)] = 0.0;
+      double un;
+      if (i == 0) un = (ny <= jin) ? c.u_ref : 0.0;
+      else if (i == nx) un = u[at(g, ny, nx - 1)];
+      else un = u[at(g, ny, i)];
+      u[at(g, ny + 1, i)] = -un;
+    }
+  }
+}
+
+// backwards_step-01.cpp:654-682: zero the faces between solid and fluid
+// cells, restated per face over the box that can border the solid block.
+__global__ void bc_step_faces_kernel(Geo g, Coef c, double* __restrict__ u, double* __restrict__ v, int box_i1,
+                                     int box_j0) {
+  const int nx = g.nx, ny = g.ny;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // 0..box_i1
+  const int j = box_j0 + blockIdx.y;
+  if (i > box_i1 || j > g.wj1 || j < g.wj0) return;
+  // u face (j, i), 1 <= j <= ny, 1 <= i <= nx-1 (interior faces the rule can touch)
+  if (j >= 1 && j <= ny && i >= 1 && i <= nx - 1) {
+    const bool a = is_fluid(c, nx, ny, j, i), b = is_fluid(c, nx, ny, j, i + 1);
+    // solid (j,i) with fluid east neighbour, or solid (j,i+1) with fluid west neighbour
+    if ((!a && b) || (!b && a)) u[at(g, j, i)] = 0.0;
+  }
+  // v face (j, i), 1 <= j <= ny-1
+  if (j >= 1 && j <= ny - 1 && i >= 1 && i <= nx) {
+    const bool a = is_fluid(c, nx, ny, j, i), b = is_fluid(c, nx, ny, j + 1, i);
+    if ((!a && b) || (!b && a)) v[at(g, j, i)] = 0.0;
+  }
+}
+
+// ------------------------------------------------------------ predictor --
+
+// cavity-01.cpp:548-603 / channel-01.cpp:546-603 / backwards_step-01.cpp:745-820.
+__global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const double* __restrict__ u,
+                                                        const double* __restrict__ v, double* __restrict__ us,
+                                                        double* __restrict__ vs) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int nx = g.nx, ny = g.ny;
+  if (j > g.j1 || j < 1 || j > ny) return;
+  const bool step = c.case_id == BACKSTEP;
+  const size_t o = at(g, j, i);
+  const size_t P = (size_t)g.pitch;
+  if (i >= 1 && i <= nx - 1) {
+    const double cc = u[o];
+    const double uE = u[o + 1], uW = u[o - 1];
+    const double uN = u[o + P], uS = u[o - P];
+    const double diff = c.nu * ((uE - 2.0 * cc + uW) * c.idx2 + (uN - 2.0 * cc + uS) * c.idy2);
+    const double ue = 0.5 * (cc + uE);
+    const double uw = 0.5 * (uW + cc);
+    const double cx = (ue * ue - uw * uw) * c.idx;
+    const double vn = 0.5 * (v[o] + v[o + 1]);
+    const double vso = 0.5 * (v[o - P] + v[o - P + 1]);
+    const double un = 0.5 * (uN + cc);
+    const double uso = 0.5 * (uS + cc);
+    const double cy = (vn * un - vso * uso) * c.idy;
+    const double val = cc + c.dt * (diff - cx - cy);
+    const bool valid = !step || is_fluid(c, nx, ny, j, i) || is_fluid(c, nx, ny, j, i + 1);
+    us[o] = valid ? val : 0.0;
+  }
+  if (i >= 1 && i <= nx && j <= ny - 1) {
+    const double cc = v[o];
+    const double vE = v[o + 1], vW = v[o - 1];
+    const double vN = v[o + P], vS = v[o - P];
+    const double diff = c.nu * ((vE - 2.0 * cc + vW) * c.idx2 + (vN - 2.0 * cc + vS) * c.idy2);
+    const double vn = 0.5 * (cc + vN);
+    const double vso = 0.5 * (vS + cc);
+    const double cy = (vn * vn - vso * vso) * c.idy;
+    const double ue = 0.5 * (u[o] + u[o + P]);
+    const double uw = 0.5 * (u[o - 1] + u[o + P - 1]);
+    const double ve = 0.5 * (cc + vE);
+    const double vw = 0.5 * (vW + cc);
+    const double cx = (ue * ve - uw * vw) * c.idx;
+    const double val = cc + c.dt * (diff - cy - cx);
+    const bool valid = !step || is_fluid(c, nx, ny, j, i) || is_fluid(c, nx, ny, j + 1, i);
+    vs[o] = valid ? val : 0.0;
+  }
+}
+
+// --------------------------------------------------------------- source --
+
+// cavity-01.cpp:622-630; channel-01.cpp:613-619 and backwards_step-01.cpp:830-841
+// (f and, for the open cases, its per-block partial sum for the mean).
+// Straight-line form: the address is formed once and the value selected, so
+// no lane's store depends on which branch the wave took.
+__global__ __launch_bounds__(256) void source_kernel(Geo g, Coef c, const double* __restrict__ us,
+                                                     const double* __restrict__ vs, double* __restrict__ f,
+                                                     double* __restrict__ partials) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int nx = g.nx, ny = g.ny;
+  const bool inside = i >= 1 && i <= nx && j >= 1 && j <= ny && j <= g.j1;
+  double val = 0.0;
+  if (inside) {
+    const size_t o = at(g, j, i);
+    const double du = us[o] - us[o - 1];
+    const double dv = vs[o] - vs[o - (size_t)g.pitch];
+    const double cav = c.cav_src * (du * c.idx + dv * c.idx);
+    const double opn = c.open_src * (du * c.idx + dv * c.idy);
+    const bool fl = is_fluid(c, nx, ny, j, i);
+    val = (c.case_id == CAVITY) ? cav : (fl ? opn : 0.0);
+    f[o] = val;
+  }
+  if (c.case_id != CAVITY) {
+    const double s = block_sum<256>(val);
+    if (threadIdx.x == 0) partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+// Sum of per-block partials in a fixed order (one block).
+__global__ __launch_bounds__(256) void sum_partials_kernel(const double* __restrict__ partials, int n,
+                                                           double* __restrict__ out) {
+  double s = 0.0;
+  for (int k = threadIdx.x; k < n; k += 256) s += partials[k];
+  s = block_sum<256>(s);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+// channel-01.cpp:621-628 / backwards_step-01.cpp:844-865: subtract the mean
+// over fluid cells.
+__global__ __launch_bounds__(256) void subtract_mean_kernel(Geo g, Coef c, double* __restrict__ f,
+                                                            const double* __restrict__ total, double count) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int nx = g.nx, ny = g.ny;
+  if (i >= 1 && i <= nx && j >= 1 && j <= ny && j <= g.j1 && is_fluid(c, nx, ny, j, i)) {
+    const double mean = total[0] / count;
+    f[at(g, j, i)] = f[at(g, j, i)] - mean;
+  }
+}
+
+// max|f| over the fluid cells the solve iterates on: cavity-01.cpp:628,
+// channel-01.cpp:643-646, backwards_step-01.cpp:880-887.
+__global__ __launch_bounds__(256) void srcmax_kernel(Geo g, Coef c, const double* __restrict__ f,
+                                                     double* __restrict__ srcmax) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int nx = g.nx, ny = g.ny;
+  double m = 0.0;
+  if (i >= 1 && i <= nx && j >= 1 && j <= ny && j <= g.j1 && is_fluid(c, nx, ny, j, i)) m = fabs(f[at(g, j, i)]);
+  block_max_to_shard<256>(m, srcmax, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
+}
+
+// Tolerance of the solve from max|f| (cavity-01.cpp:632, channel-01.cpp:647,
+// backwards_step-01.cpp:888) and the value the loop is primed with
+// (cavity-01.cpp:618: 1.0; channel-01.cpp:649: tol + 1).
+__global__ void tol_kernel(Coef c, const double* __restrict__ srcmax, double* __restrict__ tol) {
+  if (threadIdx.x != 0) return;
+  double m = 0.0;
+  for (int k = 0; k < RES_SHARDS; ++k) m = fmax(m, srcmax[k * SHARD_STRIDE]);
+  if (c.case_id == CAVITY) {
+    tol[0] = c.tol_factor * m;
+    tol[1] = 1.0;
+  } else {
+    double t = c.tol_factor * (m > 0 ? m : 1.0);
+    if (t < c.abs_tol) t = c.abs_tol;
+    tol[0] = t;
+    tol[1] = t + 1.0;
+  }
+}
+
+// ------------------------------------------------------------- Poisson --
+//
+// One red-black SOR iteration of the reference's pressure equation, fused
+// into one launch: load a (BY+2H) x (BX+2H) tile of p and the matching f tile
+// into LDS, update red cells on tile+3, black cells on tile+2, refresh the
+// ghost / solid cells on tile+1 (channel-01.cpp:531-541,
+// backwards_step-01.cpp:685-740 — after the sweep, as the reference does),
+// then compute the max-norm residual on the tile and write it out. The
+// overlapping halos are recomputed redundantly, so one launch reads p and f
+// once and writes p once (24 B per cell) and the residual needs no second
+// pass. p_in / p_out ping-pong, so tiles never read a neighbour's new values.
+//
+// SOR updates: cavity-01.cpp:643-654 (indicator form), channel-01.cpp:659-666
+// / backwards_step-01.cpp:900-909 (anisotropic form). Residuals:
+// cavity-01.cpp:659-677, channel-01.cpp:672-681, backwards_step-01.cpp:916-930.
+
+template <int CASE>
+__device__ __forceinline__ double sor_update(const Coef& c, int nx, int ny, int j, int i, double pc, double pW,
+                                             double pE, double pS, double pN, double fc) {
+  if (CASE == CAVITY) {
+    const int ew = (i > 1) ? 1 : 0;
+    const int ee = (i < nx) ? 1 : 0;
+    const int en = (j < ny) ? 1 : 0;
+    const int es = 1;
+    const int nc = ew + ee + en + es;
+    return pc * (1.0 - c.omega) +
+           (c.omega / nc) * ((ee * pE + ew * pW) + (en * pN + es * pS) - fc * c.h2);
+  } else {
+    const double sum = c.idx2 * (pE + pW) + c.idy2 * (pN + pS);
+    const double gs = (sum - fc) / c.denom;
+    return (1.0 - c.omega) * pc + c.omega * gs;
+  }
+}
+
+template <int CASE>
+__device__ __forceinline__ double residual_at(const Coef& c, int nx, int ny, int j, int i, double pc, double pW,
+                                              double pE, double pS, double pN, double fc) {
+  if (CASE == CAVITY) {
+    const int ew = (i > 1) ? 1 : 0, ee = (i < nx) ? 1 : 0, en = (j < ny) ? 1 : 0, es = 1;
+    const double ih2 = c.idx2;
+    return ih2 * (ee * (pE - pc) + ew * (pW - pc) + en * (pN - pc) + es * (pS - pc)) - fc;
+  } else {
+    const double lap = (pE - 2.0 * pc + pW) * c.idx2 + (pN - 2.0 * pc + pS) * c.idy2;
+    return lap - fc;
+  }
+}
+
+template <int CASE, int BX, int BY>
+struct PoissonTile {
+  static constexpr int H = (CASE == CAVITY) ? 3 : 4;  // cavity has no ghost refresh
+  static constexpr int LW = BX + 2 * H;
+  static constexpr int LH = BY + 2 * H;
+  static constexpr int FW = LW - 2;  // f on tile + (H-1)
+  static constexpr int FH = LH - 2;
+};
+
+template <int CASE, int BX, int BY>
+__global__ __launch_bounds__(256) void poisson_rbsor_kernel(Geo g, Coef c, const double* __restrict__ pin,
+                                                            double* __restrict__ pout,
+                                                            const double* __restrict__ f, PoissonCtl ctl,
+                                                            int k) {
+  using T = PoissonTile<CASE, BX, BY>;
+  constexpr int H = T::H, LW = T::LW, LH = T::LH, FW = T::FW, FH = T::FH;
+  constexpr int NT = 256;
+  __shared__ double sp[LH * LW];
+  __shared__ double sf[FH * FW];
+  __shared__ int s_active;
+
+  const int tid = threadIdx.x;
+  const int nx = g.nx, ny = g.ny;
+
+  // ---- convergence test of the previous iteration (reference loop condition) ----
+  if (tid < 64) {
+    const double tol = ctl.tol[0];
+    const bool stopped = ctl.stop[0] != 0;
+    const bool check = (k == 1) || ((k - 1) % ctl.check_every == 0);
+    bool active;
+    if (stopped) {
+      active = false;
+    } else if (!check) {
+      active = true;
+    } else {
+      double prev;
+      if (k == 1) {
+        prev = ctl.tol[1];
+      } else {
+        const double* slot = ctl.ring + (size_t)((k - 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+        prev = (tid < RES_SHARDS) ? slot[tid * SHARD_STRIDE] : 0.0;
+        prev = wave_max(prev);
+      }
+      active = prev > tol;
+      if (!active && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+        ctl.stop[1] = k - 1;
+        ctl.stop[0] = 1;
+      }
+    }
+    if (tid == 0) s_active = active ? 1 : 0;
+  }
+  __syncthreads();
+  if (!s_active) return;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid < RES_SHARDS) {
+    // clear the slot iteration k+1 accumulates into (k-1's slot stays readable)
+    ctl.ring[(size_t)((k + 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + tid * SHARD_STRIDE] = 0.0;
+  }
+
+  const int ti0 = blockIdx.x * BX;            // global column of tile origin
+  const int tj0 = g.wj0 + blockIdx.y * BY;    // global row of tile origin
+  const int li0 = ti0 - H, lj0 = tj0 - H;     // global coords of LDS (0,0)
+  // rows that exist in storage and in the physical grid
+  const int rmin = max(g.row_lo, 0), rmax = min(g.row_lo + g.nrows - 1, ny + 1);
+
+  // ---- stage p (tile+H) and f (tile+H-1) in LDS ----
+  for (int e = tid; e < LH * LW; e += NT) {
+    const int r = e / LW, q = e - r * LW;
+    const int gj = lj0 + r, gi = li0 + q;
+    double val = 0.0;
+    if (gj >= rmin && gj <= rmax && gi >= 0 && gi <= nx + 1) val = pin[at(g, gj, gi)];
+    sp[e] = val;
+  }
+  for (int e = tid; e < FH * FW; e += NT) {
+    const int r = e / FW, q = e - r * FW;
+    const int gj = lj0 + 1 + r, gi = li0 + 1 + q;
+    double val = 0.0;
+    if (gj >= rmin && gj <= rmax && gi >= 0 && gi <= nx + 1) val = f[at(g, gj, gi)];
+    sf[e] = val;
+  }
+  __syncthreads();
+
+  // ---- red (color 0) on tile+H-1, black (color 1) on tile+H-2 ----
+#pragma unroll
+  for (int color = 0; color < 2; ++color) {
+    const int m = H - 1 - color;            // margin around the tile
+    const int rw = BX + 2 * m, rh = BY + 2 * m;
+    const int half = (rw + 1) / 2;
+    for (int e = tid; e < rh * half; e += NT) {
+      const int r = e / half, q = e - r * half;
+      const int gj = tj0 - m + r;
+      const int gstart = ti0 - m;
+      const int par = (color - gstart - gj) & 1;  // (gi + gj) & 1 == color
+      const int qq = par + 2 * q;
+      if (qq >= rw) continue;
+      const int gi = gstart + qq;
+      if (!is_fluid(c, nx, ny, gj, gi)) continue;
+      if (gj < rmin + 1 || gj > rmax - 1) continue;  // needs both vertical neighbours stored
+      const int lr = gj - lj0, lq = gi - li0;
+      const int o = lr * LW + lq;
+      const double fc = sf[(lr - 1) * FW + (lq - 1)];
+      sp[o] = sor_update<CASE>(c, nx, ny, gj, gi, sp[o], sp[o - 1], sp[o + 1], sp[o - LW], sp[o + LW], fc);
+    }
+    __syncthreads();
+  }
+
+  // ---- ghost / solid refresh on tile+1 (open cases) ----
+  if (CASE != CAVITY) {
+    constexpr int RW = BX + 2, RH = BY + 2;
+    constexpr int NR = (RW * RH + NT - 1) / NT;
+    // only tiles whose tile+1 region touches a ghost layer or the solid block
+    const bool touches = (ti0 - 1 <= 0) || (ti0 + BX >= nx + 1) || (tj0 - 1 <= 0) || (tj0 + BY >= ny + 1) ||
+                         (CASE == BACKSTEP && ti0 - 1 <= c.step_i && tj0 + BY >= c.inlet_jmax + 1);
+    if (touches) {
+      double nv[NR];
+      int no[NR];
+#pragma unroll
+      for (int s = 0; s < NR; ++s) {
+        no[s] = -1;
+        nv[s] = 0.0;
+        const int e = tid + s * NT;
+        if (e >= RW * RH) continue;
+        const int r = e / RW, q = e - r * RW;
+        const int gj = tj0 - 1 + r, gi = ti0 - 1 + q;
+        if (gj < rmin || gj > rmax || gi < 0 || gi > nx + 1) continue;
+        const int o = (gj - lj0) * LW + (gi - li0);
+        const bool jin = gj >= 1 && gj <= ny, iin = gi >= 1 && gi <= nx;
+        if (gi == 0 && jin) {
+          nv[s] = sp[o + 1]; no[s] = o;                 // inlet Neumann
+        } else if (gi == nx + 1 && jin) {
+          nv[s] = 0.0; no[s] = o;                       // outlet Dirichlet
+        } else if (gj == 0 && iin) {
+          nv[s] = sp[o + LW]; no[s] = o;                // bottom wall Neumann
+        } else if (gj == ny + 1 && iin) {
+          nv[s] = sp[o - LW]; no[s] = o;                // top wall Neumann
+        } else if (CASE == BACKSTEP && jin && iin && !is_fluid(c, nx, ny, gj, gi)) {
+          double sum = 0.0;
+          int n = 0;
+          if (gi > 1 && is_fluid(c, nx, ny, gj, gi - 1)) { sum += sp[o - 1]; n++; }
+          if (gi < nx && is_fluid(c, nx, ny, gj, gi + 1)) { sum += sp[o + 1]; n++; }
+          if (gj > 1 && is_fluid(c, nx, ny, gj - 1, gi)) { sum += sp[o - LW]; n++; }
+          if (gj < ny && is_fluid(c, nx, ny, gj + 1, gi)) { sum += sp[o + LW]; n++; }
+          if (n > 0) { nv[s] = sum / n; no[s] = o; }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < NR; ++s)
+        if (no[s] >= 0) sp[no[s]] = nv[s];
+    }
+    __syncthreads();
+  }
+
+  // ---- residual on the tile + write-out ----
+  double rmaxv = 0.0;
+  for (int e = tid; e < BY * BX; e += NT) {
+    const int r = e / BX, q = e - r * BX;
+    const int gj = tj0 + r, gi = ti0 + q;
+    if (gj > g.wj1 || gi > nx + 1) continue;
+    const int o = (gj - lj0) * LW + (gi - li0);
+    const double pc = sp[o];
+    pout[at(g, gj, gi)] = pc;
+    if (gj >= g.j0 && gj <= g.j1 && is_fluid(c, nx, ny, gj, gi)) {
+      const int lr = gj - lj0, lq = gi - li0;
+      const double fc = sf[(lr - 1) * FW + (lq - 1)];
+      const double rv = residual_at<CASE>(c, nx, ny, gj, gi, pc, sp[o - 1], sp[o + 1], sp[o - LW], sp[o + LW], fc);
+      rmaxv = fmax(rmaxv, fabs(rv));
+    }
+  }
+  double* slot = ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+  block_max_to_shard<NT>(rmaxv, slot, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
+}
+
+// ------------------------------------------------------------ corrector --
+
+// cavity-01.cpp:695-711 / channel-01.cpp:693-702 / backwards_step-01.cpp:944-976.
+__global__ __launch_bounds__(256) void correct_kernel(Geo g, Coef c, const double* __restrict__ p,
+                                                      const double* __restrict__ us, const double* __restrict__ vs,
+                                                      double* __restrict__ u, double* __restrict__ v) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int nx = g.nx, ny = g.ny;
+  if (j > g.j1 || j < 1 || j > ny) return;
+  const bool step = c.case_id == BACKSTEP, cav = c.case_id == CAVITY;
+  const size_t o = at(g, j, i);
+  const size_t P = (size_t)g.pitch;
+  if (i >= 1 && i <= nx - 1) {
+    const double dp = p[o + 1] - p[o];
+    const double a = us[o] - c.cav_corr * dp;
+    const double b = us[o] - c.open_cu * dp;
+    const bool valid = !step || (i == nx - 1) || is_fluid(c, nx, ny, j, i) || is_fluid(c, nx, ny, j, i + 1);
+    u[o] = cav ? a : (valid ? b : 0.0);
+  }
+  if (i >= 1 && i <= nx && j <= ny - 1) {
+    const double dp = p[o + P] - p[o];
+    const double a = vs[o] - c.cav_corr * dp;
+    const double b = vs[o] - c.open_cv * dp;
+    const bool valid = !step || (j == ny - 1) || is_fluid(c, nx, ny, j, i) || is_fluid(c, nx, ny, j + 1, i);
+    v[o] = cav ? a : (valid ? b : 0.0);
+  }
+}
+
+// ------------------------------------------------------ post-processing --
+
+// cavity-01.cpp:717-733 / backwards_step-01.cpp:981-1009 (cell-centre
+// velocities) fused with cavity-01.cpp:750-764 / channel-01.cpp:743-757
+// (kinetic-energy partial sums and max |div|).
+__global__ __launch_bounds__(256) void centers_stats_kernel(Geo g, Coef c, const double* __restrict__ u,
+                                                            const double* __restrict__ v, double* __restrict__ uc,
+                                                            double* __restrict__ vc, double* __restrict__ ke_part,
+                                                            double* __restrict__ divmax) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int nx = g.nx, ny = g.ny;
+  double ke = 0.0, dv = 0.0;
+  if (i >= 1 && i <= nx && j >= 1 && j <= ny && j <= g.j1) {
+    const bool fl = is_fluid(c, nx, ny, j, i);
+    const size_t o = at(g, j, i);
+    const size_t P = (size_t)g.pitch;
+    const double uo = u[o], uw = u[o - 1], vo = v[o], vs_ = v[o - P];
+    const double a = 0.5 * (uw + uo);
+    const double b = 0.5 * (vs_ + vo);
+    const double dc = (uo - uw + vo - vs_) * c.idx;
+    const double dop = (uo - uw) * c.idx + (vo - vs_) * c.idy;
+    ke = fl ? 0.5 * (a * a + b * b) : 0.0;
+    dv = fl ? fabs(c.case_id == CAVITY ? dc : dop) : 0.0;
+    uc[o] = fl ? a : 0.0;
+    vc[o] = fl ? b : 0.0;
+  }
+  const int blin = blockIdx.y * gridDim.x + blockIdx.x;
+  const double s = block_sum<256>(ke);
+  if (threadIdx.x == 0) ke_part[blin] = s;
+  __syncthreads();
+  block_max_to_shard<256>(dv, divmax, blin % RES_SHARDS);
+}
+
+}  // namespace cfd

@@ -1,0 +1,96 @@
+// params.cpp — the reference's constants and constructor-derived quantities,
+// with the drop-in CLI overrides (--Re/--Nx/--Ny/--dt).
+//
+// Constants: cavity-01.cpp:309-320, channel-01.cpp:287-300,
+// backwards_step-01.cpp:319-334. Derivations: cavity-01.cpp:355-363,
+// channel-01.cpp:336-344, backwards_step-01.cpp:377-387; SOR factor:
+// cavity-01.cpp:74-78 / channel-01.cpp:76-81 (identical for nx == ny).
+// Mirrors cfd_amd/params.py (checked equal in tests/test_host_logic.py).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "internal.hpp"
+
+namespace {
+
+double omega_2d(int nx, int ny) {
+  const double pi = 3.14159265358979323846;
+  const double rho_j = 0.5 * (std::cos(pi / (nx + 1)) + std::cos(pi / (ny + 1)));
+  const double denom = 1.0 + std::sqrt(std::max(1e-14, 1.0 - rho_j * rho_j));
+  return 2.0 / denom;
+}
+
+}  // namespace
+
+extern "C" int cfd_params_init(int case_id, double re, int nx, int ny, double dt, cfd_params* out) {
+  if (!out) {
+    cfd::set_last_error("null output");
+    return CFD_E_ARG;
+  }
+  cfd_params p;
+  std::memset(&p, 0, sizeof p);
+  p.case_id = case_id;
+  p.check_every = 1;
+  p.chunk = 0;
+  switch (case_id) {
+    case CFD_CAVITY:
+      p.nx = p.ny = 63; p.length = 1.0; p.height = 1.0; p.re = 1000.0; p.u_ref = 1.0; p.rho = 1.0;
+      p.cfl = 0.5; p.final_time = 20.0; p.tol_factor = 1e-9; p.abs_tol = 0.0; p.max_iters = 10000;
+      p.print_interval = 100; p.save_interval = 100;
+      break;
+    case CFD_CHANNEL:
+      p.nx = 93; p.ny = 31; p.length = 3.0; p.height = 1.0; p.re = 100.0; p.u_ref = 1.0; p.rho = 1.0;
+      p.cfl = 0.25; p.final_time = 10.0; p.tol_factor = 1e-7; p.abs_tol = 1e-10; p.max_iters = 10000;
+      p.print_interval = 100; p.save_interval = 100;
+      break;
+    case CFD_BACKSTEP:
+      p.nx = 256; p.ny = 32; p.length = 8.0; p.height = 2.0; p.re = 100.0; p.u_ref = 1.0; p.rho = 1.0;
+      p.cfl = 0.2; p.final_time = 15.0; p.tol_factor = 1e-7; p.abs_tol = 1e-10; p.max_iters = 10000;
+      p.print_interval = 10; p.save_interval = 10; p.h_inlet = 1.0; p.step_x = 2.0;
+      break;
+    default:
+      cfd::set_last_error("unknown case_id");
+      return CFD_E_ARG;
+  }
+  if (re > 0) p.re = re;
+  if (nx > 0) p.nx = nx;
+  if (ny > 0) p.ny = ny;
+  else if (nx > 0 && case_id == CFD_CAVITY) p.ny = nx;
+  if (p.nx < 2 || p.ny < 2) {
+    cfd::set_last_error("grid must have at least 2 interior cells per direction");
+    return CFD_E_ARG;
+  }
+  if (case_id == CFD_CAVITY) {
+    p.height = p.ny * p.length / p.nx;
+    p.nu = p.rho * p.u_ref * p.length / p.re;
+    p.dx = p.dy = p.length / p.nx;
+    const double h = p.dx;
+    p.dt = p.cfl * std::min(0.25 * h * h / p.nu, h / p.u_ref);
+  } else {
+    p.nu = p.u_ref * (case_id == CFD_CHANNEL ? p.height : p.h_inlet) / p.re;
+    p.dx = p.length / p.nx;
+    p.dy = p.height / p.ny;
+    const double h = std::min(p.dx, p.dy);
+    p.dt = p.cfl * std::min(0.25 * h * h / p.nu, h / std::max(1e-12, p.u_ref));
+  }
+  if (dt > 0) p.dt = dt;
+  p.omega = omega_2d(p.nx, p.ny);
+  p.total_steps = (int)(p.final_time / p.dt);
+  if (case_id == CFD_BACKSTEP) {
+    p.step_i = (int)(p.step_x / p.dx);
+    p.inlet_jmax = (int)(p.h_inlet / p.dy);
+    if (p.step_i <= 0 || p.step_i >= p.nx) {
+      cfd::set_last_error("Step location is outside computational domain!");
+      return CFD_E_ARG;
+    }
+  } else {
+    p.inlet_jmax = p.ny;
+  }
+  if (!(p.dt > 0)) {
+    cfd::set_last_error("Computed time step is non-positive. Check physical parameters!");
+    return CFD_E_ARG;
+  }
+  *out = p;
+  return CFD_OK;
+}

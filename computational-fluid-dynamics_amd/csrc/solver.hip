@@ -1,0 +1,676 @@
+// solver.hip — host orchestration of the MI355X projection solver and the
+// C-ABI of libcfd_amd.so (include/cfd_amd.h).
+//
+// One Solver object = the reference's CavitySolver / ChannelSolver /
+// BackwardsStepSolver (cavity-01.cpp:306, channel-01.cpp:284,
+// backwards_step-01.cpp:316): device-resident fields, the per-timestep
+// methods as kernel launches on one HIP stream, and the SOR loop driven from
+// the host with the convergence test evaluated on the device (no host sync
+// per iteration). The grid may be split into row strips — several on one
+// device (halo copies on the stream) or one per rank (halo rows over RCCL).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "internal.hpp"
+#include "kernels.hpp"
+
+namespace cfd {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& m) { g_last_error = m; }
+
+#define HIPC(x)                                                                                  \
+  do {                                                                                           \
+    hipError_t e_ = (x);                                                                         \
+    if (e_ != hipSuccess) throw Error(CFD_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+static void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw Error(CFD_E_DEVICE, std::string("launch ") + what + ": " + hipGetErrorString(e));
+}
+
+enum { B_P0 = 0, B_P1, B_F, B_US, B_VS, B_U, B_V, B_UC, B_VC, NB };
+
+constexpr int PBX = 64, PBY = 32;  // Poisson tile
+
+struct Strip {
+  Geo g{};
+  double* b[NB] = {};
+  dim3 grid2d;          // 64 x 4 blocks over owned interior rows
+  size_t part_off = 0;  // offset into the partial-sum buffer
+};
+
+static Coef make_coef(const cfd_params& p) {
+  Coef c{};
+  c.case_id = p.case_id;
+  c.step_i = p.step_i;
+  c.inlet_jmax = p.inlet_jmax;
+  c.dx = p.dx;
+  c.dy = p.dy;
+  c.idx = 1.0 / p.dx;
+  c.idy = 1.0 / p.dy;
+  c.idx2 = 1.0 / (p.dx * p.dx);
+  c.idy2 = 1.0 / (p.dy * p.dy);
+  c.nu = p.nu;
+  c.dt = p.dt;
+  c.rho = p.rho;
+  c.u_ref = p.u_ref;
+  c.omega = p.omega;
+  c.h2 = p.dx * p.dx;
+  c.denom = 2.0 * (c.idx2 + c.idy2);
+  c.cav_src = (1.0 / p.dt) * p.rho;
+  c.open_src = p.rho / p.dt;
+  c.cav_corr = (p.dt / p.dx) * p.rho;
+  c.open_cu = p.dt / (p.rho * p.dx);
+  c.open_cv = p.dt / (p.rho * p.dy);
+  c.tol_factor = p.tol_factor;
+  c.abs_tol = p.abs_tol;
+  return c;
+}
+
+class Solver {
+ public:
+  cfd_params P{};
+  Coef C{};
+  int dev = 0;
+  hipStream_t st = nullptr;
+  std::vector<Strip> S;
+  Comm* comm = nullptr;  // non-null: this process is one rank of a strip decomposition
+  int pcur = 0;          // which p buffer holds the current pressure
+  int pitch = 0;
+  double fluid_count = 0;
+
+  double *ring = nullptr, *srcmax = nullptr, *divmax = nullptr, *tolv = nullptr, *partials = nullptr,
+         *total = nullptr;
+  int* stop = nullptr;
+  size_t npart = 0;
+  int* h_stat = nullptr;    // pinned: 2 x {stop, iter}
+  double* h_shard = nullptr;  // pinned: RES_SHARDS*SHARD_STRIDE
+  hipEvent_t ev_poll[2] = {}, ev_a = nullptr, ev_b = nullptr;
+  cfd_timing T{};
+
+  Solver(const cfd_params& p, int device, const std::vector<std::pair<int, int>>& rows, Comm* cm)
+      : P(p), dev(device), comm(cm) {
+    validate();
+    C = make_coef(P);
+    HIPC(hipSetDevice(dev));
+    hipDeviceProp_t prop;
+    HIPC(hipGetDeviceProperties(&prop, dev));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      throw Error(CFD_E_DEVICE, std::string("libcfd_amd requires gfx950 (MI355X); device is ") + prop.gcnArchName);
+    HIPC(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    pitch = ((P.nx + 2) + 15) / 16 * 16;
+    size_t part = 0;
+    for (auto [j0, j1] : rows) {
+      Strip s;
+      Geo& g = s.g;
+      g.nx = P.nx;
+      g.ny = P.ny;
+      g.pitch = pitch;
+      g.j0 = j0;
+      g.j1 = j1;
+      g.wj0 = (j0 == 1) ? 0 : j0;
+      g.wj1 = (j1 == P.ny) ? P.ny + 1 : j1;
+      g.row_lo = j0 - HALO;
+      g.nrows = (j1 - j0 + 1) + 2 * HALO;
+      const size_t n = (size_t)g.nrows * (size_t)pitch;
+      for (int k = 0; k < NB; ++k) {
+        HIPC(hipMalloc(&s.b[k], n * sizeof(double)));
+        HIPC(hipMemsetAsync(s.b[k], 0, n * sizeof(double), st));
+      }
+      s.grid2d = dim3((P.nx + 2 + 63) / 64, (j1 - j0 + 1 + 3) / 4);
+      s.part_off = part;
+      part += (size_t)s.grid2d.x * s.grid2d.y;
+      S.push_back(s);
+    }
+    npart = part;
+    const size_t ringn = (size_t)RING * RES_SHARDS * SHARD_STRIDE;
+    HIPC(hipMalloc(&ring, ringn * sizeof(double)));
+    HIPC(hipMalloc(&srcmax, RES_SHARDS * SHARD_STRIDE * sizeof(double)));
+    HIPC(hipMalloc(&divmax, RES_SHARDS * SHARD_STRIDE * sizeof(double)));
+    HIPC(hipMalloc(&tolv, 2 * sizeof(double)));
+    HIPC(hipMalloc(&total, 4 * sizeof(double)));
+    HIPC(hipMalloc(&partials, std::max<size_t>(npart, 1) * sizeof(double)));
+    HIPC(hipMalloc(&stop, 2 * sizeof(int)));
+    HIPC(hipMemsetAsync(ring, 0, ringn * sizeof(double), st));
+    HIPC(hipMemsetAsync(tolv, 0, 2 * sizeof(double), st));
+    HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
+    HIPC(hipHostMalloc(&h_stat, 4 * sizeof(int), hipHostMallocDefault));
+    HIPC(hipHostMalloc(&h_shard, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipHostMallocDefault));
+    for (auto& e : ev_poll) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPC(hipEventCreate(&ev_a));
+    HIPC(hipEventCreate(&ev_b));
+    // fluid cells (backwards_step-01.cpp:522-528)
+    long long solid = 0;
+    if (P.case_id == CFD_BACKSTEP)
+      solid = (long long)std::min(P.step_i, P.nx) * (long long)std::max(0, P.ny - P.inlet_jmax);
+    fluid_count = (double)((long long)P.nx * P.ny - solid);
+    // channel-01.cpp:352 / backwards_step-01.cpp:396: constructor applies the velocity BCs
+    if (P.case_id != CFD_CAVITY) apply_bc(false);
+    HIPC(hipStreamSynchronize(st));
+  }
+
+  ~Solver() {
+    (void)hipSetDevice(dev);
+    if (st) (void)hipStreamSynchronize(st);
+    for (auto& s : S)
+      for (auto* p : s.b) (void)hipFree(p);
+    for (double* p : {ring, srcmax, divmax, tolv, total, partials}) (void)hipFree(p);
+    (void)hipFree(stop);
+    (void)hipHostFree(h_stat);
+    (void)hipHostFree(h_shard);
+    for (auto& e : ev_poll)
+      if (e) (void)hipEventDestroy(e);
+    if (ev_a) (void)hipEventDestroy(ev_a);
+    if (ev_b) (void)hipEventDestroy(ev_b);
+    if (st) (void)hipStreamDestroy(st);
+  }
+
+  void validate() const {
+    if (P.case_id < 0 || P.case_id > 2) throw Error(CFD_E_ARG, "unknown case_id");
+    if (P.nx < 2 || P.ny < 2) throw Error(CFD_E_ARG, "grid must have at least 2 interior cells per direction");
+    if (!(P.dx > 0) || !(P.dy > 0) || !(P.dt > 0) || !(P.nu > 0) || !(P.rho > 0))
+      throw Error(CFD_E_ARG, "dx, dy, dt, nu and rho must be positive");
+    if (!(P.omega > 0) || !(P.omega < 2)) throw Error(CFD_E_ARG, "SOR omega must lie in (0, 2)");
+    if (P.max_iters < 0) throw Error(CFD_E_ARG, "max_iters must be >= 0");
+    if (P.check_every < 1) throw Error(CFD_E_ARG, "check_every must be >= 1");
+    if (P.case_id == CFD_BACKSTEP && (P.step_i <= 0 || P.step_i >= P.nx))
+      throw Error(CFD_E_ARG, "Step location is outside computational domain!");
+    if (P.case_id == CFD_BACKSTEP && (P.inlet_jmax < 1 || P.inlet_jmax > P.ny))
+      throw Error(CFD_E_ARG, "inlet height is outside computational domain");
+  }
+
+  bool multi() const { return S.size() > 1 || comm != nullptr; }
+
+  // ------------------------------------------------------------ halos --
+  // Copy `depth` owned boundary rows of buffer b into the neighbours' halos.
+  void exchange(int b, int depth) {
+    if (S.size() > 1) {
+      for (size_t k = 0; k + 1 < S.size(); ++k) {
+        Strip& lo = S[k];
+        Strip& up = S[k + 1];
+        const size_t cnt = (size_t)depth * pitch * sizeof(double);
+        const int ja = lo.g.j1 - depth + 1;  // lower strip's top rows -> upper's lower halo
+        HIPC(hipMemcpyAsync(up.b[b] + (size_t)(ja - up.g.row_lo) * pitch, lo.b[b] + (size_t)(ja - lo.g.row_lo) * pitch,
+                            cnt, hipMemcpyDeviceToDevice, st));
+        const int jb = up.g.j0;  // upper strip's bottom rows -> lower's upper halo
+        HIPC(hipMemcpyAsync(lo.b[b] + (size_t)(jb - lo.g.row_lo) * pitch, up.b[b] + (size_t)(jb - up.g.row_lo) * pitch,
+                            cnt, hipMemcpyDeviceToDevice, st));
+      }
+    }
+    if (comm && comm->nranks > 1) {
+      Strip& s = S[0];
+      const Geo& g = s.g;
+      double* base = s.b[b];
+      const size_t cnt = (size_t)depth * pitch;
+      auto row = [&](int j) { return base + (size_t)(j - g.row_lo) * pitch; };
+      comm_group_start();
+      if (comm->rank > 0) {
+        comm_send(comm, row(g.j0), cnt, comm->rank - 1, st);
+        comm_recv(comm, row(g.j0 - depth), cnt, comm->rank - 1, st);
+      }
+      if (comm->rank < comm->nranks - 1) {
+        comm_send(comm, row(g.j1 - depth + 1), cnt, comm->rank + 1, st);
+        comm_recv(comm, row(g.j1 + 1), cnt, comm->rank + 1, st);
+      }
+      comm_group_end();
+    }
+  }
+
+  // ------------------------------------------------------------- phases --
+  void apply_bc(bool tentative) {
+    const int bu = tentative ? B_US : B_U, bv = tentative ? B_VS : B_V;
+    for (auto& s : S) {
+      const Geo& g = s.g;
+      const int n = std::max(P.nx + 1, g.wj1 - g.wj0 + 1);
+      const dim3 grid((n + 255) / 256);
+      if (P.case_id == CFD_CAVITY) {
+        if (tentative) continue;  // the cavity never applies BCs to u*, v*
+        bc_cavity_kernel<<<grid, 256, 0, st>>>(g, C, s.b[bu], s.b[bv]);
+        check_launch("bc_cavity");
+      } else {
+        bc_open_kernel<<<grid, 256, 0, st>>>(g, C, s.b[bu], s.b[bv]);
+        check_launch("bc_open");
+        if (P.case_id == CFD_BACKSTEP) {
+          const int box_i1 = std::min(P.step_i + 1, P.nx);
+          const int box_j0 = std::max(P.inlet_jmax, g.wj0);
+          const int box_j1 = std::min(P.ny, g.wj1);
+          if (box_j1 >= box_j0) {
+            const dim3 gf((box_i1 + 1 + 63) / 64, box_j1 - box_j0 + 1);
+            bc_step_faces_kernel<<<gf, 64, 0, st>>>(g, C, s.b[bu], s.b[bv], box_i1, box_j0);
+            check_launch("bc_step_faces");
+          }
+        }
+      }
+    }
+  }
+
+  void compute_tentative() {
+    if (multi()) {
+      exchange(B_U, 1);
+      exchange(B_V, 1);
+    }
+    for (auto& s : S) {
+      tentative_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_U], s.b[B_V], s.b[B_US], s.b[B_VS]);
+      check_launch("tentative");
+    }
+  }
+
+  void build_source() {
+    if (multi()) exchange(B_VS, 1);
+    for (auto& s : S) {
+      source_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_US], s.b[B_VS], s.b[B_F], partials + s.part_off);
+      check_launch("source");
+    }
+    if (P.case_id != CFD_CAVITY) {
+      sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total);
+      check_launch("sum_partials");
+      if (comm && comm->nranks > 1) comm_allreduce_sum(comm, total, 1, st);
+      for (auto& s : S) {
+        subtract_mean_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_F], total, fluid_count);
+        check_launch("subtract_mean");
+      }
+    }
+  }
+
+  // Tolerance from the current source (computed inside the reference's solve).
+  void solve_tolerance() {
+    HIPC(hipMemsetAsync(srcmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
+    for (auto& s : S) {
+      srcmax_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_F], srcmax);
+      check_launch("srcmax");
+    }
+    if (comm && comm->nranks > 1) comm_allreduce_max(comm, srcmax, RES_SHARDS * SHARD_STRIDE, st);
+    tol_kernel<<<1, 64, 0, st>>>(C, srcmax, tolv);
+    check_launch("tol");
+  }
+
+  template <int CASE>
+  void launch_poisson(const double* const* pin, double* const* pout, int k) {
+    PoissonCtl ctl{ring, tolv, stop, P.check_every};
+    for (size_t q = 0; q < S.size(); ++q) {
+      const Geo& g = S[q].g;
+      const dim3 grid((P.nx + 2 + PBX - 1) / PBX, (g.wj1 - g.wj0 + 1 + PBY - 1) / PBY);
+      poisson_rbsor_kernel<CASE, PBX, PBY><<<grid, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k);
+    }
+    check_launch("poisson_rbsor");
+  }
+
+  void poisson_iteration(int k, int base) {
+    const int bin = ((base + k - 1) & 1) ? B_P1 : B_P0;
+    const int bout = ((base + k) & 1) ? B_P1 : B_P0;
+    if (multi()) exchange(bin, HALO);
+    std::vector<const double*> pin(S.size());
+    std::vector<double*> pout(S.size());
+    for (size_t q = 0; q < S.size(); ++q) {
+      pin[q] = S[q].b[bin];
+      pout[q] = S[q].b[bout];
+    }
+    if (P.case_id == CFD_CAVITY) launch_poisson<CAVITY>(pin.data(), pout.data(), k);
+    else if (P.case_id == CFD_CHANNEL) launch_poisson<CHANNEL>(pin.data(), pout.data(), k);
+    else launch_poisson<BACKSTEP>(pin.data(), pout.data(), k);
+    if (comm && comm->nranks > 1 && (k % P.check_every == 0 || k == P.max_iters)) {
+      double* slot = ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+      comm_allreduce_max(comm, slot, RES_SHARDS * SHARD_STRIDE, st);
+    }
+  }
+
+  // solverPressurePoisson (cavity-01.cpp:609-690, channel-01.cpp:635-688,
+  // backwards_step-01.cpp:872-939). Requires build_source() first.
+  void solve(cfd_step_info* out) {
+    const int base = pcur;
+    HIPC(hipMemsetAsync(ring, 0, (size_t)RING * RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
+    HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
+    if (P.case_id == CFD_CAVITY) {
+      // cavity-01.cpp:610-611: each solve starts from a zero field
+      for (auto& s : S)
+        HIPC(hipMemsetAsync(s.b[base ? B_P1 : B_P0], 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
+    }
+    solve_tolerance();
+    if (multi()) exchange(B_F, HALO - 1);
+    const int chunk = P.chunk > 0 ? P.chunk : 32;
+    HIPC(hipEventRecord(ev_a, st));
+    int k = 0, c = 0;
+    bool stopped = false;
+    while (k < P.max_iters && !stopped) {
+      const int n = std::min(chunk, P.max_iters - k);
+      for (int j = 1; j <= n; ++j) poisson_iteration(k + j, base);
+      k += n;
+      HIPC(hipMemcpyAsync(h_stat + 2 * (c & 1), stop, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPC(hipEventRecord(ev_poll[c & 1], st));
+      if (c > 0) {
+        HIPC(hipEventSynchronize(ev_poll[(c - 1) & 1]));
+        if (h_stat[2 * ((c - 1) & 1)] != 0) stopped = true;
+      }
+      ++c;
+    }
+    HIPC(hipEventRecord(ev_b, st));
+    int iters;
+    if (c > 0) {
+      HIPC(hipEventSynchronize(ev_poll[(c - 1) & 1]));
+      const int* hs = h_stat + 2 * ((c - 1) & 1);
+      iters = hs[0] ? hs[1] : P.max_iters;
+    } else {
+      iters = 0;
+    }
+    HIPC(hipEventSynchronize(ev_b));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
+    T.poisson_ms += ms;
+    T.poisson_launches += k;
+    long long owned = 0;
+    for (auto& s : S) owned += (long long)(s.g.j1 - s.g.j0 + 1) * P.nx;
+    T.poisson_cell_updates += owned * iters;
+    double res;
+    if (iters == 0) {
+      double t2[2];
+      HIPC(hipMemcpy(t2, tolv, sizeof t2, hipMemcpyDeviceToHost));
+      res = t2[1];
+    } else {
+      const double* slot = ring + (size_t)(iters & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+      HIPC(hipMemcpy(h_shard, slot, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost));
+      res = 0.0;
+      for (int q = 0; q < RES_SHARDS; ++q) res = std::max(res, h_shard[q * SHARD_STRIDE]);
+    }
+    pcur = (base + iters) & 1;
+    if (out) {
+      out->sor_iterations = iters;
+      out->residual = res;
+    }
+  }
+
+  void correct() {
+    const int bp = pcur ? B_P1 : B_P0;
+    if (multi()) exchange(bp, 1);
+    for (auto& s : S) {
+      correct_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_US], s.b[B_VS], s.b[B_U], s.b[B_V]);
+      check_launch("correct");
+    }
+  }
+
+  // run() loop body: cavity-01.cpp:387-390; channel-01.cpp:368-375.
+  void step(cfd_step_info* out) {
+    if (P.case_id == CFD_CAVITY) {
+      apply_bc(false);
+      compute_tentative();
+      build_source();
+      solve(out);
+      correct();
+    } else {
+      compute_tentative();
+      apply_bc(true);
+      build_source();
+      solve(out);
+      correct();
+      apply_bc(false);
+    }
+    T.steps += 1;
+  }
+
+  void stats(cfd_stats* out) {
+    if (multi()) exchange(B_V, 1);
+    HIPC(hipMemsetAsync(divmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
+    for (auto& s : S) {
+      centers_stats_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_U], s.b[B_V], s.b[B_UC], s.b[B_VC],
+                                                       partials + s.part_off, divmax);
+      check_launch("centers_stats");
+    }
+    sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total + 1);
+    check_launch("sum_partials");
+    if (comm && comm->nranks > 1) {
+      comm_allreduce_sum(comm, total + 1, 1, st);
+      comm_allreduce_max(comm, divmax, RES_SHARDS * SHARD_STRIDE, st);
+    }
+    double ke = 0;
+    HIPC(hipMemcpyAsync(h_shard, divmax, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(&ke, total + 1, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    double md = 0;
+    for (int q = 0; q < RES_SHARDS; ++q) md = std::max(md, h_shard[q * SHARD_STRIDE]);
+    if (out) {
+      out->max_divergence = md;
+      out->avg_kinetic_energy = ke / fluid_count;
+    }
+  }
+
+  // ------------------------------------------------------ field access --
+  int field_buf(int field) const {
+    switch (field) {
+      case CFD_FIELD_P: return pcur ? B_P1 : B_P0;
+      case CFD_FIELD_SRC: return B_F;
+      case CFD_FIELD_US: return B_US;
+      case CFD_FIELD_VS: return B_VS;
+      case CFD_FIELD_U: return B_U;
+      case CFD_FIELD_V: return B_V;
+      case CFD_FIELD_UC: return B_UC;
+      case CFD_FIELD_VC: return B_VC;
+    }
+    throw Error(CFD_E_ARG, "unknown field");
+  }
+  void field_dims(int field, int& rows, int& cols) const {
+    rows = P.ny + 2;
+    cols = P.nx + 2;
+    if (field == CFD_FIELD_U || field == CFD_FIELD_US) cols = P.nx + 1;
+    if (field == CFD_FIELD_V || field == CFD_FIELD_VS) rows = P.ny + 1;
+  }
+  // rows of `field` stored by this solver: [first, last] (global)
+  void owned_field_rows(int field, int& first, int& last) const {
+    int rows, cols;
+    field_dims(field, rows, cols);
+    first = S.front().g.wj0;
+    last = std::min(S.back().g.wj1, rows - 1);
+  }
+
+  void transfer(int field, double* host, const double* chost, size_t count) {
+    int rows, cols, first, last;
+    field_dims(field, rows, cols);
+    owned_field_rows(field, first, last);
+    if (count != (size_t)(last - first + 1) * cols) throw Error(CFD_E_ARG, "host buffer size does not match field shape");
+    const int b = field_buf(field);
+    for (auto& s : S) {
+      const int r0 = s.g.wj0, r1 = std::min(s.g.wj1, rows - 1);
+      if (r1 < r0) continue;
+      double* dev = s.b[b] + (size_t)(r0 - s.g.row_lo) * pitch;
+      const size_t hoff = (size_t)(r0 - first) * cols;
+      if (host)
+        HIPC(hipMemcpy2DAsync(host + hoff, cols * sizeof(double), dev, pitch * sizeof(double), cols * sizeof(double),
+                              r1 - r0 + 1, hipMemcpyDeviceToHost, st));
+      else
+        HIPC(hipMemcpy2DAsync(dev, pitch * sizeof(double), chost + hoff, cols * sizeof(double), cols * sizeof(double),
+                              r1 - r0 + 1, hipMemcpyHostToDevice, st));
+    }
+    HIPC(hipStreamSynchronize(st));
+  }
+
+  void write_vtk(const std::string& fn, double t) {
+    if (comm && comm->nranks > 1) throw Error(CFD_E_STATE, "cfd_write_vtk needs the whole grid (single-rank solver)");
+    cfd_stats tmp;
+    stats(&tmp);  // refreshes the cell-centre fields
+    const size_t n = (size_t)(P.ny + 2) * (P.nx + 2);
+    std::vector<double> uc(n), vc(n), pr(n);
+    transfer(CFD_FIELD_UC, uc.data(), nullptr, n);
+    transfer(CFD_FIELD_VC, vc.data(), nullptr, n);
+    transfer(CFD_FIELD_P, pr.data(), nullptr, n);
+    write_vtk_arrays(P, fn, t, uc.data(), vc.data(), pr.data());
+  }
+};
+
+}  // namespace cfd
+
+// =================================================================== C-ABI ==
+
+using cfd::Error;
+using cfd::Solver;
+
+struct cfd_solver {
+  Solver* impl;
+};
+
+template <class F>
+static int guard(F&& f) {
+  try {
+    f();
+    return CFD_OK;
+  } catch (const Error& e) {
+    cfd::set_last_error(e.what());
+    return e.code;
+  } catch (const std::exception& e) {
+    cfd::set_last_error(e.what());
+    return CFD_E_DEVICE;
+  } catch (...) {
+    cfd::set_last_error("unknown error");
+    return CFD_E_DEVICE;
+  }
+}
+
+static Solver* S_(cfd_solver* s) {
+  if (!s || !s->impl) throw Error(CFD_E_ARG, "null solver");
+  HIPC(hipSetDevice(s->impl->dev));
+  return s->impl;
+}
+
+extern "C" {
+
+int cfd_abi_version(void) { return CFD_AMD_ABI_VERSION; }
+const char* cfd_last_error(void) { return cfd::g_last_error.c_str(); }
+
+cfd_solver* cfd_create(const cfd_params* p, int device, int n_strips) {
+  cfd_solver* out = nullptr;
+  guard([&] {
+    if (!p) throw Error(CFD_E_ARG, "null params");
+    if (n_strips < 1) throw Error(CFD_E_ARG, "n_strips must be >= 1");
+    if (p->ny < n_strips * cfd::HALO) throw Error(CFD_E_ARG, "each strip needs at least 4 rows");
+    std::vector<std::pair<int, int>> rows;
+    for (int k = 0; k < n_strips; ++k) {
+      const int a = 1 + (int)((long long)p->ny * k / n_strips);
+      const int b = (int)((long long)p->ny * (k + 1) / n_strips);
+      rows.emplace_back(a, b);
+    }
+    out = new cfd_solver{new Solver(*p, device, rows, nullptr)};
+  });
+  return out;
+}
+
+cfd_solver* cfd_create_rank(const cfd_params* p, int device, int row_begin, int row_end, void* comm) {
+  cfd_solver* out = nullptr;
+  guard([&] {
+    if (!p) throw Error(CFD_E_ARG, "null params");
+    if (row_begin < 1 || row_end > p->ny || row_end - row_begin + 1 < cfd::HALO)
+      throw Error(CFD_E_ARG, "rank rows must lie in [1, ny] and span at least 4 rows");
+    out = new cfd_solver{new Solver(*p, device, {{row_begin, row_end}}, static_cast<cfd::Comm*>(comm))};
+  });
+  return out;
+}
+
+int cfd_destroy(cfd_solver* s) {
+  return guard([&] {
+    if (!s) return;
+    delete s->impl;
+    delete s;
+  });
+}
+
+int cfd_apply_bc(cfd_solver* s) { return guard([&] { S_(s)->apply_bc(false); }); }
+int cfd_apply_tentative_bc(cfd_solver* s) { return guard([&] { S_(s)->apply_bc(true); }); }
+int cfd_compute_tentative(cfd_solver* s) { return guard([&] { S_(s)->compute_tentative(); }); }
+int cfd_build_source(cfd_solver* s) { return guard([&] { S_(s)->build_source(); }); }
+int cfd_solve_pressure(cfd_solver* s, cfd_step_info* out) { return guard([&] { S_(s)->solve(out); }); }
+int cfd_apply_correction(cfd_solver* s) { return guard([&] { S_(s)->correct(); }); }
+int cfd_step(cfd_solver* s, cfd_step_info* out) { return guard([&] { S_(s)->step(out); }); }
+int cfd_run_steps(cfd_solver* s, int n, cfd_step_info* last) {
+  return guard([&] {
+    Solver* v = S_(s);
+    cfd_step_info info{0, 0.0};
+    for (int k = 0; k < n; ++k) v->step(&info);
+    if (last) *last = info;
+  });
+}
+int cfd_compute_stats(cfd_solver* s, cfd_stats* out) { return guard([&] { S_(s)->stats(out); }); }
+
+int cfd_field_shape(const cfd_solver* s, int field, int* rows, int* cols) {
+  return guard([&] {
+    if (!s || !s->impl || !rows || !cols) throw Error(CFD_E_ARG, "null argument");
+    int r, c, first, last;
+    s->impl->field_dims(field, r, c);
+    s->impl->owned_field_rows(field, first, last);
+    *rows = last - first + 1;
+    *cols = c;
+  });
+}
+
+int cfd_get_field(cfd_solver* s, int field, double* host, size_t count) {
+  return guard([&] {
+    if (!host) throw Error(CFD_E_ARG, "null host buffer");
+    S_(s)->transfer(field, host, nullptr, count);
+  });
+}
+
+int cfd_set_field(cfd_solver* s, int field, const double* host, size_t count) {
+  return guard([&] {
+    if (!host) throw Error(CFD_E_ARG, "null host buffer");
+    S_(s)->transfer(field, nullptr, host, count);
+  });
+}
+
+int cfd_write_vtk(cfd_solver* s, const char* filename, double t) {
+  return guard([&] {
+    if (!filename) throw Error(CFD_E_ARG, "null filename");
+    S_(s)->write_vtk(filename, t);
+  });
+}
+
+int cfd_write_vtk_arrays(const cfd_params* p, const char* filename, double t, const double* uc, const double* vc,
+                         const double* pr) {
+  return guard([&] {
+    if (!p || !filename || !uc || !vc || !pr) throw Error(CFD_E_ARG, "null argument");
+    cfd::write_vtk_arrays(*p, filename, t, uc, vc, pr);
+  });
+}
+
+int cfd_write_pvd(const char* filename, const char* const* files, const double* times, int n) {
+  return guard([&] {
+    if (!filename || n < 0 || (n > 0 && (!files || !times))) throw Error(CFD_E_ARG, "bad arguments");
+    cfd::write_pvd(filename, files, times, n);
+  });
+}
+
+int cfd_get_timing(cfd_solver* s, cfd_timing* out) {
+  return guard([&] {
+    if (!out) throw Error(CFD_E_ARG, "null output");
+    *out = S_(s)->T;
+  });
+}
+int cfd_reset_timing(cfd_solver* s) { return guard([&] { S_(s)->T = cfd_timing{}; }); }
+int cfd_synchronize(cfd_solver* s) { return guard([&] { HIPC(hipStreamSynchronize(S_(s)->st)); }); }
+
+int cfd_owned_rows(const cfd_solver* s, int* first, int* last) {
+  return guard([&] {
+    if (!s || !s->impl || !first || !last) throw Error(CFD_E_ARG, "null argument");
+    *first = s->impl->S.front().g.j0;
+    *last = s->impl->S.back().g.j1;
+  });
+}
+
+int cfd_comm_unique_id(unsigned char* id_out) {
+  return guard([&] {
+    if (!id_out) throw Error(CFD_E_ARG, "null id");
+    cfd::comm_unique_id(id_out);
+  });
+}
+
+void* cfd_comm_init(const unsigned char* id, int nranks, int rank, int device) {
+  void* out = nullptr;
+  guard([&] {
+    if (!id) throw Error(CFD_E_ARG, "null id");
+    out = cfd::comm_init(id, nranks, rank, device);
+  });
+  return out;
+}
+
+int cfd_comm_destroy(void* comm) { return guard([&] { cfd::comm_destroy(static_cast<cfd::Comm*>(comm)); }); }
+
+}  // extern "C"

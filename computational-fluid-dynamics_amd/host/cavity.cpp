@@ -1,0 +1,4 @@
+// cavity.cpp — drop-in for the reference's ./cavity binary (see driver.hpp).
+#include "driver.hpp"
+
+int main(int argc, char** argv) { return host::run_case(CFD_CAVITY, argc, argv); }

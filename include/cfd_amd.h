@@ -1,0 +1,160 @@
+/*
+ * include/cfd_amd.h — C-ABI of libcfd_amd.so, the MI355X-native projection
+ * solver (lid-driven cavity, channel, backwards-facing step).
+ *
+ * The reference has no FFI: each case is one C++ class driven by main()
+ * (cavity-01.cpp:306-775, channel-01.cpp:284-770, backwards_step-01.cpp:316-1062).
+ * The entry points below are that class's per-timestep methods, exported with
+ * plain pointers and sizes so a host in any language can bind them. Each
+ * declaration names the reference method it replaces. All functions return
+ * 0 on success and a negative CFD_E_* code on failure; cfd_last_error()
+ * then describes the failure. No function falls back to a CPU path: if no
+ * usable gfx950 device is present, cfd_create fails.
+ */
+#ifndef CFD_AMD_H
+#define CFD_AMD_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CFD_AMD_ABI_VERSION 1
+
+enum cfd_case { CFD_CAVITY = 0, CFD_CHANNEL = 1, CFD_BACKSTEP = 2 };
+
+/* Fields, named after the reference members (cavity-01.cpp:336-344). */
+enum cfd_field {
+  CFD_FIELD_P = 0,    /* pressure            (ny+2) x (nx+2) */
+  CFD_FIELD_SRC = 1,  /* source_term         (ny+2) x (nx+2) */
+  CFD_FIELD_US = 3,   /* u_tentative         (ny+2) x (nx+1) */
+  CFD_FIELD_VS = 4,   /* v_tentative         (ny+1) x (nx+2) */
+  CFD_FIELD_U = 5,    /* u_corrected         (ny+2) x (nx+1) */
+  CFD_FIELD_V = 6,    /* v_corrected         (ny+1) x (nx+2) */
+  CFD_FIELD_UC = 7,   /* u_center            (ny+2) x (nx+2) */
+  CFD_FIELD_VC = 8    /* v_center            (ny+2) x (nx+2) */
+};
+
+enum {
+  CFD_OK = 0,
+  CFD_E_ARG = -1,      /* invalid argument */
+  CFD_E_DEVICE = -2,   /* HIP runtime / device failure */
+  CFD_E_COMM = -3,     /* RCCL failure */
+  CFD_E_STATE = -4,    /* call not valid in the current state */
+  CFD_E_IO = -5        /* file output failure */
+};
+
+/*
+ * Solver parameters: the reference's derived constants (cavity-01.cpp:322-327,
+ * channel-01.cpp:302-308, backwards_step-01.cpp:337-352). Hosts derive them
+ * from the CLI with cfd_params_init(); all fields may then be overridden.
+ */
+typedef struct cfd_params {
+  int case_id;          /* enum cfd_case */
+  int nx, ny;           /* global interior cells */
+  double length, height;
+  double re, u_ref, rho, cfl, final_time;
+  double dx, dy, nu, dt, omega;
+  double tol_factor, abs_tol;
+  int max_iters;        /* MAX_SOR_ITERS */
+  int total_steps;
+  int print_interval, save_interval;
+  double h_inlet, step_x;  /* backwards step geometry */
+  int step_i, inlet_jmax;  /* derived step indices (backwards_step-01.cpp:386, 493) */
+  int check_every;      /* residual test every N SOR iterations (1 = reference) */
+  int chunk;            /* SOR launches enqueued between host polls (0 = auto) */
+} cfd_params;
+
+typedef struct cfd_solver cfd_solver;
+
+typedef struct cfd_step_info {
+  int sor_iterations;   /* SolverResult.first  (cavity-01.cpp:689) */
+  double residual;      /* SolverResult.second (max-norm PPE residual) */
+} cfd_step_info;
+
+typedef struct cfd_stats {
+  double max_divergence;      /* logStatistics, cavity-01.cpp:757-764 */
+  double avg_kinetic_energy;  /* logStatistics, cavity-01.cpp:750-766 */
+} cfd_stats;
+
+typedef struct cfd_timing {
+  double poisson_ms;          /* device time inside SOR launches (HIP events) */
+  long long poisson_launches; /* SOR kernel launches that did work */
+  long long poisson_cell_updates; /* interior cells x active iterations (this rank) */
+  double step_ms;             /* device time of whole timesteps */
+  long long steps;
+} cfd_timing;
+
+/* Library / ABI info. */
+int cfd_abi_version(void);
+const char* cfd_last_error(void);
+
+/* Reference constants for a case with CLI overrides (<=0 / NULL keeps the
+ * reference value): the constructor initialisers of the reference classes
+ * (cavity-01.cpp:355-364, channel-01.cpp:336-345, backwards_step-01.cpp:377-388). */
+int cfd_params_init(int case_id, double re, int nx, int ny, double dt, cfd_params* out);
+
+/* Construct a solver: CavitySolver()/ChannelSolver()/BackwardsStepSolver()
+ * (cavity-01.cpp:355, channel-01.cpp:336, backwards_step-01.cpp:377) —
+ * allocateFields + setupGeometry + the initial applyBoundaryConditions of the
+ * open cases. The grid is split into `n_strips` row strips on this device
+ * (1 = one domain); strips exchange halo rows after every stage. */
+cfd_solver* cfd_create(const cfd_params* p, int device, int n_strips);
+
+/* Multi-process construction: this rank owns interior rows
+ * [row_begin, row_end] (1-based, inclusive) of the global grid; neighbour
+ * halos travel over RCCL (see cfd_comm_*). */
+cfd_solver* cfd_create_rank(const cfd_params* p, int device, int row_begin, int row_end, void* comm);
+int cfd_destroy(cfd_solver* s);
+
+/* Per-timestep methods. */
+int cfd_apply_bc(cfd_solver* s);                  /* applyBoundaryConditions   cavity-01.cpp:523 / channel-01.cpp:509 */
+int cfd_apply_tentative_bc(cfd_solver* s);        /* applyVelocityBC(u*,v*)    channel-01.cpp:369 */
+int cfd_compute_tentative(cfd_solver* s);         /* computeTentativeVelocities cavity-01.cpp:548 */
+int cfd_build_source(cfd_solver* s);              /* source term (+ mean removal) cavity-01.cpp:622 / channel-01.cpp:608 */
+int cfd_solve_pressure(cfd_solver* s, cfd_step_info* out); /* solverPressurePoisson cavity-01.cpp:609 */
+int cfd_apply_correction(cfd_solver* s);          /* applyPressureCorrection   cavity-01.cpp:695 */
+int cfd_step(cfd_solver* s, cfd_step_info* out);  /* one iteration of run()'s loop, cavity-01.cpp:387-390 */
+int cfd_run_steps(cfd_solver* s, int n_steps, cfd_step_info* last); /* n loop iterations, no logging */
+
+/* interpolateToCellCenters + logStatistics reductions (cavity-01.cpp:717, 741). */
+int cfd_compute_stats(cfd_solver* s, cfd_stats* out);
+
+/* Field transfer in the reference's array shapes (see enum cfd_field), as
+ * dense row-major doubles: rows x cols with rows/cols from cfd_field_shape.
+ * For a rank solver only the rank's owned rows are transferred. */
+int cfd_field_shape(const cfd_solver* s, int field, int* rows, int* cols);
+int cfd_get_field(cfd_solver* s, int field, double* host, size_t count);
+int cfd_set_field(cfd_solver* s, int field, const double* host, size_t count);
+
+/* VTKWriter::write_structured_grid (cavity-01.cpp:95-231; masked variant
+ * backwards_step-01.cpp:102-243) and write_paraview_collection
+ * (cavity-01.cpp:255-287). */
+int cfd_write_vtk(cfd_solver* s, const char* filename, double time_value);
+int cfd_write_pvd(const char* filename, const char* const* vtk_files, const double* times, int n);
+
+/* Host-only VTK formatting of given cell-centre / pressure arrays, each a
+ * dense (ny+2) x (nx+2) row-major array in the reference's indexing. */
+int cfd_write_vtk_arrays(const cfd_params* p, const char* filename, double time_value, const double* u_center,
+                         const double* v_center, const double* pressure);
+
+/* Interior rows [first, last] (global, 1-based) this solver owns. */
+int cfd_owned_rows(const cfd_solver* s, int* first, int* last);
+
+/* Timing collected with HIP events on the solver's stream. */
+int cfd_get_timing(cfd_solver* s, cfd_timing* out);
+int cfd_reset_timing(cfd_solver* s);
+int cfd_synchronize(cfd_solver* s);
+
+/* RCCL bootstrap for multi-process strip decomposition: rank 0 creates an id
+ * (opaque bytes, CFD_COMM_ID_BYTES), every rank passes it to cfd_comm_init. */
+#define CFD_COMM_ID_BYTES 128
+int cfd_comm_unique_id(unsigned char* id_out);
+void* cfd_comm_init(const unsigned char* id, int nranks, int rank, int device);
+int cfd_comm_destroy(void* comm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,288 @@
+"""GPU parity: libcfd_amd.so (HIP kernels) against the CPU oracle.
+
+Bars:
+  * stencil phases (BCs, predictor, source, corrector): bit-exact;
+  * SOR solve: bit-exact against the oracle's red-black restatement (same
+    iteration count, same field); against the reference's lexicographic
+    ordering the converged fields agree to the solver tolerance;
+  * whole runs: centerline u/v within 1e-6 relative L2 of the reference
+    algorithm (north_star), bit-exact against the red-black oracle for the
+    cavity (no reductions feed the state);
+  * strip decomposition: identical to one domain (cavity bit-exact; the open
+    cases' mean-removal sum is re-associated, so 1e-12).
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+import cfd_amd as C  # noqa: E402
+import oracle as O  # noqa: E402
+
+CASES = ["cavity", "channel", "backwards_step"]
+
+
+def small_params(case: str, **kw):
+    if case == "cavity":
+        return C.make_params(case, **kw)
+    if case == "channel":
+        return C.make_params(case, **kw)
+    return C.make_params(case, **kw)
+
+
+def ofield(o, name, cp):
+    """Oracle field cut to the reference shape of `name`."""
+    a = o.field(name)
+    if name in ("u", "us"):
+        return a[:, : cp.nx + 1]
+    if name in ("v", "vs"):
+        return a[: cp.ny + 1, :]
+    return a
+
+
+def set_both(g, o, name, value, cp):
+    g.set_field(name, value)
+    ofield(o, name, cp)[...] = value
+
+
+def assert_bits(a, b, what):
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert a.shape == b.shape, what
+    bad = np.argwhere(a.view(np.int64) != b.view(np.int64))
+    if bad.size:
+        j, i = bad[0]
+        raise AssertionError(f"{what}: {len(bad)} cells differ, first at (j={j}, i={i}): gpu={a[j, i]!r} "
+                             f"oracle={b[j, i]!r}")
+
+
+def centerlines(u_c, v_c, cp):
+    """u along the vertical centreline, v along the horizontal one (cell centres)."""
+    ic = (cp.nx + 1) // 2
+    jc = (cp.ny + 1) // 2
+    return u_c[1:cp.ny + 1, ic], v_c[jc, 1:cp.nx + 1]
+
+
+def rel_l2(a, b):
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+@pytest.mark.parametrize("strips", [1, 3])
+@pytest.mark.parametrize("case", CASES)
+def test_stencil_phases_bitexact(case, strips):
+    cp = small_params(case)
+    g = C.solver_for(cp, n_strips=strips)
+    o = O.Oracle(cp)
+    rng = np.random.default_rng(1234)
+    nx, ny = cp.nx, cp.ny
+    set_both(g, o, "u", rng.standard_normal((ny + 2, nx + 1)), cp)
+    set_both(g, o, "v", rng.standard_normal((ny + 1, nx + 2)), cp)
+
+    g.applyBoundaryConditions()
+    o.velocity_bc(False)
+    assert_bits(g.field("u"), ofield(o, "u", cp), "BC u")
+    assert_bits(g.field("v"), ofield(o, "v", cp), "BC v")
+
+    g.computeTentativeVelocities()
+    o.tentative()
+    assert_bits(g.field("us"), ofield(o, "us", cp), "tentative u*")
+    assert_bits(g.field("vs"), ofield(o, "vs", cp), "tentative v*")
+
+    if case != "cavity":
+        g.applyTentativeBoundaryConditions()
+        o.velocity_bc(True)
+        assert_bits(g.field("us"), ofield(o, "us", cp), "BC u*")
+        assert_bits(g.field("vs"), ofield(o, "vs", cp), "BC v*")
+
+    g.buildSourceTerm()
+    o.source()
+    if case == "cavity":
+        assert_bits(g.field("src"), o.field("src"), "source")
+    else:  # mean removal: tree sum vs sequential sum
+        np.testing.assert_allclose(g.field("src"), o.field("src"), rtol=0, atol=1e-12 * np.abs(o.field("src")).max())
+
+    pr = rng.standard_normal((ny + 2, nx + 2))
+    set_both(g, o, "p", pr, cp)
+    set_both(g, o, "us", rng.standard_normal((ny + 2, nx + 1)), cp)
+    set_both(g, o, "vs", rng.standard_normal((ny + 1, nx + 2)), cp)
+    g.applyPressureCorrection()
+    o.correct()
+    assert_bits(g.field("u"), ofield(o, "u", cp), "corrected u")
+    assert_bits(g.field("v"), ofield(o, "v", cp), "corrected v")
+
+    md, ke = g.statistics()
+    omd, oke = o.stats()
+    assert md == omd
+    assert ke == pytest.approx(oke, rel=1e-12)
+    assert_bits(g.field("uc"), o.field("uc"), "u_center")
+    assert_bits(g.field("vc"), o.field("vc"), "v_center")
+
+
+@pytest.mark.parametrize("strips", [1, 2])
+@pytest.mark.parametrize("case", CASES)
+def test_poisson_rb_bitexact(case, strips):
+    """The fused red-black kernel == the oracle's red-black restatement, bit for bit."""
+    cp = small_params(case, max_iters=3000)
+    g = C.solver_for(cp, n_strips=strips)
+    o = O.Oracle(cp, ordering=O.RB)
+    rng = np.random.default_rng(7)
+    nx, ny = cp.nx, cp.ny
+    f = np.zeros((ny + 2, nx + 2))
+    f[1:ny + 1, 1:nx + 1] = rng.standard_normal((ny, nx)) * 10.0
+    if case == "backwards_step":
+        f[o.mask() == 0] = 0.0
+    f[1:ny + 1, 1:nx + 1] -= f[1:ny + 1, 1:nx + 1].mean() if case == "channel" else 0.0
+    set_both(g, o, "src", f, cp)
+    if case != "cavity":
+        set_both(g, o, "p", rng.standard_normal((ny + 2, nx + 2)) * 0.1, cp)
+    it_g, res_g = g.solverPressurePoisson()
+    it_o, res_o = o.poisson()
+    assert it_g == it_o
+    assert res_g == res_o
+    assert_bits(g.field("p"), o.field("p"), "pressure")
+
+
+@pytest.mark.parametrize("case", ["cavity", "channel"])
+def test_poisson_converges_to_reference_solution(case):
+    """Red-black vs the reference's lexicographic SOR: same fixed point to tolerance
+    (cases whose reference solve converges; see test_oracle_golden for the step)."""
+    cp = small_params(case, max_iters=10000)
+    g = C.solver_for(cp)
+    o = O.Oracle(cp, ordering=O.LEX)
+    if case != "cavity":
+        g.applyBoundaryConditions()
+    # a realistic source: one predictor step from the initial state
+    for s in (g,):
+        if case == "cavity":
+            s.applyBoundaryConditions()
+        s.computeTentativeVelocities()
+        if case != "cavity":
+            s.applyTentativeBoundaryConditions()
+        s.buildSourceTerm()
+    o.velocity_bc(False)  # cavity: step's BC; open cases: the constructor's BC
+    o.tentative()
+    if case != "cavity":
+        o.velocity_bc(True)
+    o.source()
+    it_g, res_g = g.solverPressurePoisson()
+    it_o, res_o = o.poisson()
+    pg, po = g.field("p"), o.field("p")
+    inner = (slice(1, cp.ny + 1), slice(1, cp.nx + 1))
+    scale = np.abs(po[inner]).max()
+    assert np.abs(pg[inner] - po[inner]).max() <= 1e-6 * scale, (it_g, it_o)
+
+
+@pytest.mark.parametrize("case,steps", [("cavity", 60), ("channel", 40)])
+def test_run_matches_reference_algorithm(case, steps):
+    """North-star bar: centerline u/v within 1e-6 rel-L2 of the reference algorithm.
+
+    Norm: ||gpu - ref|| / ||u_ref|| on each centerline, i.e. relative to the
+    centerline velocity scale (the channel's horizontal-centerline v is ~0 by
+    symmetry, so normalising by ||v_ref|| would measure round-off)."""
+    cp = small_params(case)
+    g = C.solver_for(cp)
+    olex = O.Oracle(cp, ordering=O.LEX)
+    orb = O.Oracle(cp, ordering=O.RB)
+    if case != "cavity":
+        olex.velocity_bc(False)
+        orb.velocity_bc(False)
+    for _ in range(steps):
+        ig, _ = g.step()
+        olex.step()
+        ir, _ = orb.step()
+        if case == "cavity":
+            assert ig == ir
+    g.statistics()
+    olex.centers()
+    orb.centers()
+    ug, vg = centerlines(g.field("uc"), g.field("vc"), cp)
+    ul, vl = centerlines(olex.field("uc"), olex.field("vc"), cp)
+    scale = np.linalg.norm(ul)
+    assert np.linalg.norm(ug - ul) / scale <= 1e-6
+    assert np.linalg.norm(vg - vl) / max(scale, np.linalg.norm(vl)) <= 1e-6
+    if case == "cavity":
+        assert_bits(g.field("u"), ofield(orb, "u", cp), "cavity run u vs red-black oracle")
+        assert_bits(g.field("v"), ofield(orb, "v", cp), "cavity run v vs red-black oracle")
+
+
+def test_backstep_run_matches_red_black_oracle():
+    """The step's reference solve never converges, so the red-black path is held
+    to its own CPU restatement (same ordering): equal up to the source-mean
+    re-association (1e-10), iteration counts equal."""
+    cp = small_params("backwards_step")
+    g = C.solver_for(cp)
+    orb = O.Oracle(cp, ordering=O.RB)
+    orb.velocity_bc(False)
+    for _ in range(3):
+        ig, _ = g.step()
+        ir, _ = orb.step()
+        assert ig == ir
+    for name in ("u", "v"):
+        ref = ofield(orb, name, cp)
+        np.testing.assert_allclose(g.field(name), ref, rtol=0, atol=1e-10 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_strips_equal_single_domain(case):
+    cp = small_params(case)
+    steps = 3 if case == "backwards_step" else 20
+    a = C.solver_for(cp, n_strips=1)
+    b = C.solver_for(cp, n_strips=4)
+    for _ in range(steps):
+        ia, _ = a.step()
+        ib, _ = b.step()
+        if case == "cavity":
+            assert ia == ib
+    for name in ("u", "v", "p"):
+        if case == "cavity":
+            assert_bits(b.field(name), a.field(name), f"strips {name}")
+        else:
+            ref = a.field(name)
+            np.testing.assert_allclose(b.field(name), ref, rtol=0, atol=1e-10 * max(np.abs(ref).max(), 1.0))
+
+
+def test_cavity_final_frame_matches_reference_output():
+    """Full reference run (63^2, Re 1000, 2520 steps) against its own VTK output."""
+    cp = C.reference_defaults("cavity")
+    g = C.CavitySolver(cp)
+    g.applyBoundaryConditions()
+    g.run_steps(cp.total_steps)
+    g.statistics()
+    F = np.load(os.path.join(GOLDEN, "ref_fields.npz"))
+    inner = (slice(1, cp.ny + 1), slice(1, cp.nx + 1))
+    for name, key in (("uc", "u_velocity"), ("vc", "v_velocity"), ("p", "pressure")):
+        ref = F[f"cavity/{cp.total_steps}/{key}"]
+        mine = g.field(name)[inner]
+        # reference prints 6 decimals (|rounding| <= 5e-7) + converged-SOR ordering difference
+        assert np.abs(mine - ref).max() <= 2e-6, (name, np.abs(mine - ref).max())
+    ug, vg = centerlines(g.field("uc"), g.field("vc"), cp)
+    uref = F[f"cavity/{cp.total_steps}/u_velocity"][:, (cp.nx + 1) // 2 - 1]
+    vref = F[f"cavity/{cp.total_steps}/v_velocity"][(cp.ny + 1) // 2 - 1, :]
+    assert rel_l2(ug, uref) <= 5e-6
+    assert rel_l2(vg, vref) <= 5e-6
+
+
+def test_log_lines_match_reference_format():
+    """run() prints the reference's log lines; iteration counts differ only by ordering."""
+    import io
+    cp = C.reference_defaults("channel")
+    g = C.ChannelSolver(cp)
+    out, err = io.StringIO(), io.StringIO()
+    g.run(output_directory=None, out=out, err=err, steps=200)
+    lines = out.getvalue().splitlines()
+    logs = json.load(open(os.path.join(GOLDEN, "ref_logs.json")))["channel"]["steps"][:2]
+    assert len(lines) == 2
+    for a, b in zip(lines, logs):
+        # same fields, same formatting; avg_KE agrees to within one unit of the
+        # 6th printed decimal (red-black vs lexicographic SOR, tolerance 1e-7)
+        fa, fb = a.split("|"), b.split("|")
+        assert len(fa) == len(fb) and fa[0] == fb[0] and fa[1] == fb[1]
+        ka, kb = float(fa[3].split("=")[1]), float(fb[3].split("=")[1])
+        assert abs(ka - kb) <= 1.5e-6
