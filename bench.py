@@ -193,7 +193,7 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "poisson_rbsor_kernel<cavity>",
+                "kernel": "poisson_wave_kernel<cavity>",
                 "bytes_per_launch": BYTES_PER_CELL * cells_per_launch,
                 "avg_launch_us": round(avg_launch_ms * 1e3, 2),
             },

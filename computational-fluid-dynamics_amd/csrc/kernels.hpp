@@ -40,6 +40,8 @@ struct Coef {
   double idx, idy, idx2, idy2;  // 1/dx, 1/dy, 1/(dx*dx), 1/(dy*dy)
   double nu, dt, rho, u_ref;
   double omega;
+  double one_m_omega;      // 1.0 - omega (same rounding as the reference's expression)
+  double om_nc[5];         // cavity: omega / neighbour_count for counts 0..4
   double h2;               // cavity: grid_spacing * grid_spacing
   double denom;            // open cases: 2*(idx2+idy2)
   double cav_src;          // cavity: (1/dt) * rho           (cavity-01.cpp:624)
@@ -357,12 +359,17 @@ __device__ __forceinline__ double sor_update(const Coef& c, int nx, int ny, int 
     const int en = (j < ny) ? 1 : 0;
     const int es = 1;
     const int nc = ew + ee + en + es;
-    return pc * (1.0 - c.omega) +
-           (c.omega / nc) * ((ee * pE + ew * pW) + (en * pN + es * pS) - fc * c.h2);
+    // c.om_nc[nc] == c.omega / nc and c.one_m_omega == 1.0 - c.omega, computed once on the host.
+    // Indicator products without int->double multiplies: 1*x == x and, for
+    // finite x, 0*x == copysign(0, x) — the same bits as the reference's product.
+    const double tE = ee ? pE : copysign(0.0, pE);
+    const double tW = ew ? pW : copysign(0.0, pW);
+    const double tN = en ? pN : copysign(0.0, pN);
+    return pc * c.one_m_omega + c.om_nc[nc] * ((tE + tW) + (tN + pS) - fc * c.h2);
   } else {
     const double sum = c.idx2 * (pE + pW) + c.idy2 * (pN + pS);
     const double gs = (sum - fc) / c.denom;
-    return (1.0 - c.omega) * pc + c.omega * gs;
+    return c.one_m_omega * pc + c.omega * gs;
   }
 }
 
@@ -549,6 +556,431 @@ __global__ __launch_bounds__(256) void poisson_rbsor_kernel(Geo g, Coef c, const
   }
   double* slot = ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
   block_max_to_shard<NT>(rmaxv, slot, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
+}
+
+// ------------------------------------------------ Poisson, column march --
+//
+// The same red-black SOR iteration as poisson_rbsor_kernel (identical
+// arithmetic, bit-identical results), restructured for bandwidth: a block of
+// 256 threads owns 256 consecutive columns (248 output columns + 4 halo
+// columns each side) and marches down a band of TH rows. Each thread keeps a
+// 6-row register window of its column; row neighbours come from two LDS row
+// rings. At front row R one step does
+//   load p_in(R), f(R-1)      red at row R-1      black at row R-2
+//   ghost/solid refresh at row R-3 (open cases)   residual + store at row R-4
+// and every LDS value read in a step was written in an earlier step, so one
+// barrier per row suffices. Bands overlap by 4 rows (recomputed), tiles by 4
+// columns each side. HBM traffic per cell: p_in + f read once, p_out written
+// once (24 B) plus the band/tile overlap.
+
+template <int CASE>
+__device__ __forceinline__ bool refresh_value(const Coef& c, int nx, int ny, int gj, int gi, double self,
+                                              double pW, double pE, double pS, double pN, double& out) {
+  // channel-01.cpp:531-541, backwards_step-01.cpp:685-740 (pre-refresh neighbour values)
+  if (CASE == CAVITY) return false;
+  const bool jin = gj >= 1 && gj <= ny, iin = gi >= 1 && gi <= nx;
+  if (gi == 0 && jin) { out = pE; return true; }
+  if (gi == nx + 1 && jin) { out = 0.0; return true; }
+  if (gj == 0 && iin) { out = pN; return true; }
+  if (gj == ny + 1 && iin) { out = pS; return true; }
+  if (CASE == BACKSTEP && jin && iin && !is_fluid(c, nx, ny, gj, gi)) {
+    double sum = 0.0;
+    int n = 0;
+    if (gi > 1 && is_fluid(c, nx, ny, gj, gi - 1)) { sum += pW; n++; }
+    if (gi < nx && is_fluid(c, nx, ny, gj, gi + 1)) { sum += pE; n++; }
+    if (gj > 1 && is_fluid(c, nx, ny, gj - 1, gi)) { sum += pS; n++; }
+    if (gj < ny && is_fluid(c, nx, ny, gj + 1, gi)) { sum += pN; n++; }
+    if (n > 0) { out = sum / n; return true; }
+  }
+  (void)self;
+  return false;
+}
+
+template <int CASE>
+__global__ __launch_bounds__(256) void poisson_march_kernel(Geo g, Coef c, const double* __restrict__ pin,
+                                                            double* __restrict__ pout,
+                                                            const double* __restrict__ f, PoissonCtl ctl, int k,
+                                                            int TH, int ctiles, int nbands, int flags) {
+  // flags bit 0: alternate the march direction of neighbouring bands
+  //       bit 1: XCD-aware tile order
+  constexpr int NT = 256, H = 4, TW = NT - 2 * H, NR = 4;
+  __shared__ double L[NR][NT];  // post-red/black values (pre-refresh)
+  __shared__ double F[NR][NT];  // final values (after refresh)
+  __shared__ int s_active;
+
+  const int t = threadIdx.x;
+  const int nx = g.nx, ny = g.ny;
+
+  if (t < 64) {
+    const double tol = ctl.tol[0];
+    const bool stopped = ctl.stop[0] != 0;
+    const bool check = (k == 1) || ((k - 1) % ctl.check_every == 0);
+    bool active;
+    if (stopped) {
+      active = false;
+    } else if (!check) {
+      active = true;
+    } else {
+      double prev;
+      if (k == 1) {
+        prev = ctl.tol[1];
+      } else {
+        const double* slot = ctl.ring + (size_t)((k - 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+        prev = (t < RES_SHARDS) ? slot[t * SHARD_STRIDE] : 0.0;
+        prev = wave_max(prev);
+      }
+      active = prev > tol;
+      if (!active && t == 0 && blockIdx.x == 0) {
+        ctl.stop[1] = k - 1;
+        ctl.stop[0] = 1;
+      }
+    }
+    if (t == 0) s_active = active ? 1 : 0;
+  }
+  __syncthreads();
+  if (!s_active) return;
+  if (blockIdx.x == 0 && t < RES_SHARDS)
+    ctl.ring[(size_t)((k + 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + t * SHARD_STRIDE] = 0.0;
+
+  // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin dispatch),
+  // so consecutive tile ids -- vertically adjacent bands of one column tile --
+  // are given to blocks on one XCD and read their shared halo rows from its L2.
+  const int nb = ctiles * nbands;
+  const int L8 = (nb / 8) * 8;
+  const int bl = (int)blockIdx.x;
+  const int tile = ((flags & 2) && bl < L8) ? (bl % 8) * (nb / 8) + bl / 8 : bl;
+  const int band = tile % nbands, ctile = tile / nbands;
+
+  const int gi = ctile * TW - H + t;
+  const int y0 = g.wj0 + band * TH;
+  const int y1 = min(y0 + TH, g.wj1 + 1);  // one past the last output row
+  if (y0 > g.wj1) return;                  // (uniform) empty band
+  const bool col_ok = gi >= 0 && gi <= nx + 1;
+  const bool icol = gi >= 1 && gi <= nx;
+  const bool out_col = col_ok && t >= H && t < NT - H;
+  const bool edge = (t == 0) || (t == NT - 1);
+  const bool upd_col = icol && !edge;
+  const bool step_open_col = (CASE != BACKSTEP) || (gi > c.step_i);  // fluid in every interior row
+  const int rmin = max(g.row_lo, 0), rmax = min(g.row_lo + g.nrows - 1, ny + 1);
+  const size_t P = (size_t)g.pitch;
+  // alternate march direction: a band's shared halo rows are read by both
+  // neighbours at the same time (both at their start, or both at their end)
+  const int d = ((flags & 1) && (band & 1)) ? -1 : 1;
+  const int Rbeg = (d > 0) ? y0 - H : y1 - 1 + H;
+  const int nsteps = (y1 - y0) + 2 * H;
+
+  auto fluid = [&](int j) -> bool {  // is_fluid(c, nx, ny, j, gi) with the column part hoisted
+    return icol && j >= 1 && j <= ny && (CASE != BACKSTEP || step_open_col || j <= c.inlet_jmax);
+  };
+  auto row_ok = [&](int R) -> bool { return col_ok && R >= rmin && R <= rmax; };
+  const double* prow = pin + (ptrdiff_t)(Rbeg - g.row_lo) * (ptrdiff_t)P + gi;
+  const double* frow = f + (ptrdiff_t)(Rbeg - d - g.row_lo) * (ptrdiff_t)P + gi;
+  const ptrdiff_t dP = (ptrdiff_t)d * (ptrdiff_t)P;
+
+  // register windows (march order): w<k> = post-black value of row R-(5-k)d,
+  // q<k> = final value of row R-(5-k)d; f of rows R-4d .. R-d
+  double w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
+  double q0 = 0, q1 = 0, q2 = 0;
+  double fa = 0, fb = 0, fc = 0, fd = 0;
+  double rmaxv = 0.0;
+
+  // prefetch queue: 3 rows of p_in and f in flight
+  double np1 = row_ok(Rbeg) ? prow[0] : 0.0, nf1 = row_ok(Rbeg - d) ? frow[0] : 0.0;
+  double np2 = row_ok(Rbeg + d) ? prow[dP] : 0.0, nf2 = row_ok(Rbeg) ? frow[dP] : 0.0;
+  double np3 = row_ok(Rbeg + 2 * d) ? prow[2 * dP] : 0.0, nf3 = row_ok(Rbeg + d) ? frow[2 * dP] : 0.0;
+  prow += 3 * dP;
+  frow += 3 * dP;
+
+  int R = Rbeg;
+  for (int s = 0; s < nsteps; ++s, R += d) {
+    const double pR = np1, fR = nf1;
+    np1 = np2;
+    nf1 = nf2;
+    np2 = np3;
+    nf2 = nf3;
+    np3 = row_ok(R + 3 * d) ? prow[0] : 0.0;
+    nf3 = row_ok(R + 2 * d) ? frow[0] : 0.0;
+    prow += dP;
+    frow += dP;
+    w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = pR;
+    fa = fb; fb = fc; fc = fd; fd = fR;
+    L[R & (NR - 1)][t] = pR;
+
+    // red (color 0) at row R-d: neighbours along the march w3 (behind), w5 (ahead)
+    {
+      const int j = R - d;
+      if (upd_col && ((gi + j) & 1) == 0 && fluid(j) && j > rmin && j < rmax) {
+        const double pW = L[j & (NR - 1)][t - 1], pE = L[j & (NR - 1)][t + 1];
+        const double pS = (d > 0) ? w3 : w5, pN = (d > 0) ? w5 : w3;
+        w4 = sor_update<CASE>(c, nx, ny, j, gi, w4, pW, pE, pS, pN, fd);
+        L[j & (NR - 1)][t] = w4;
+      }
+    }
+    // black (color 1) at row R-2d: w2 (behind), w4 (ahead, red-updated)
+    {
+      const int j = R - 2 * d;
+      if (upd_col && ((gi + j) & 1) == 1 && fluid(j) && j > rmin && j < rmax) {
+        const double pW = L[j & (NR - 1)][t - 1], pE = L[j & (NR - 1)][t + 1];
+        const double pS = (d > 0) ? w2 : w4, pN = (d > 0) ? w4 : w2;
+        w3 = sor_update<CASE>(c, nx, ny, j, gi, w3, pW, pE, pS, pN, fc);
+        L[j & (NR - 1)][t] = w3;
+      }
+    }
+    // refresh at row R-3d (pre-refresh neighbours: w1, w3 along the march, L[R-3d] across)
+    q0 = q1;
+    q1 = q2;
+    {
+      const int j = R - 3 * d;
+      double nv = w2;
+      if (CASE != CAVITY && !edge) {
+        double out;
+        const double pS = (d > 0) ? w1 : w3, pN = (d > 0) ? w3 : w1;
+        if (refresh_value<CASE>(c, nx, ny, j, gi, w2, L[j & (NR - 1)][t - 1], L[j & (NR - 1)][t + 1], pS, pN, out))
+          nv = out;
+      }
+      q2 = nv;
+      F[j & (NR - 1)][t] = nv;
+    }
+    // residual + store at row R-4d: q0 (behind), q2 (ahead); F[R-4d] across
+    {
+      const int j = R - 4 * d;
+      if (out_col && j >= y0 && j < y1) {
+        pout[(size_t)(j - g.row_lo) * P + gi] = q1;
+        if (j >= g.j0 && j <= g.j1 && fluid(j)) {
+          const double pW = F[j & (NR - 1)][t - 1], pE = F[j & (NR - 1)][t + 1];
+          const double pS = (d > 0) ? q0 : q2, pN = (d > 0) ? q2 : q0;
+          const double rv = residual_at<CASE>(c, nx, ny, j, gi, q1, pW, pE, pS, pN, fa);
+          rmaxv = fmax(rmaxv, fabs(rv));
+        }
+      }
+    }
+    __syncthreads();
+  }
+  double* slot = ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+  block_max_to_shard<NT>(rmaxv, slot, tile % RES_SHARDS);
+}
+
+// ---------------------------------------------- Poisson, wave march -----
+//
+// The same red-black SOR iteration again (bit-identical), with no LDS and no
+// barriers: every wave is an independent tile of 128 columns (2 per lane,
+// 16-byte loads and stores) marching down a band of rows, and row neighbours
+// across lanes move by DPP wave shifts. 4 columns each side are halo
+// (recomputed), so a wave writes 120 columns. Rows R+1..R+4 of p_in and f
+// are kept in flight in registers.
+
+__device__ __forceinline__ double dpp_from_left(double v) {  // lane l receives lane l-1 (wave_shr:1)
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xf, 0xf, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, 0x138, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_from_right(double v) {  // lane l receives lane l+1 (wave_shl:1)
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xf, 0xf, false);
+  hi = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Residual magnitude for the march kernels: as residual_at, but the cavity's
+// 0/1 indicator products are selects. Only |r| is used (max-norm), and
+// 0*x == +-0 adds nothing to a sum with a non-zero term, so |r| is identical.
+template <int CASE>
+__device__ __forceinline__ double residual_abs(const Coef& c, int nx, int ny, int j, int i, double pc, double pW,
+                                               double pE, double pS, double pN, double fc) {
+  if (CASE == CAVITY) {
+    const double tE = (i < nx) ? (pE - pc) : 0.0;
+    const double tW = (i > 1) ? (pW - pc) : 0.0;
+    const double tN = (j < ny) ? (pN - pc) : 0.0;
+    const double tS = pS - pc;
+    return fabs(c.idx2 * (tE + tW + tN + tS) - fc);
+  } else {
+    return fabs(residual_at<CASE>(c, nx, ny, j, i, pc, pW, pE, pS, pN, fc));
+  }
+}
+
+template <int CASE, int DIR, int PD, bool COPY = false>
+__device__ __forceinline__ void wave_march(const Geo& g, const Coef& c, const double* __restrict__ pin,
+                                           double* __restrict__ pout, const double* __restrict__ f, int lane,
+                                           int gi, int y0, int y1, double& rmaxv) {
+  constexpr int H = 4;
+  const int nx = g.nx, ny = g.ny;
+  const int rmin = max(g.row_lo, 0), rmax = min(g.row_lo + g.nrows - 1, ny + 1);
+  const size_t P = (size_t)g.pitch;
+  const bool pair_ok = gi >= 0 && gi + 1 < g.pitch;  // both columns stored (pitch >= nx+3)
+  const bool out_lane = pair_ok && lane >= H / 2 && lane < 64 - H / 2;
+  const bool icol_a = gi >= 1 && gi <= nx, icol_b = gi + 1 >= 1 && gi + 1 <= nx;
+  const bool open_a = (CASE != BACKSTEP) || (gi > c.step_i), open_b = (CASE != BACKSTEP) || (gi + 1 > c.step_i);
+  const int gic = min(max(gi, 0), g.pitch - 2);  // clamped column: loads always hit valid memory
+  const int Rbeg = (DIR > 0) ? y0 - H : y1 - 1 + H;
+  const int nsteps = (y1 - y0) + 2 * H;
+  auto fl_a = [&](int j) -> bool { return icol_a && j >= 1 && j <= ny && (open_a || j <= c.inlet_jmax); };
+  auto fl_b = [&](int j) -> bool { return icol_b && j >= 1 && j <= ny && (open_b || j <= c.inlet_jmax); };
+  auto ld = [&](const double* base, int R) -> double2 {
+    const int Rc = min(max(R, rmin), rmax);
+    const double2 v = *reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * P + gic);
+    const bool ok = pair_ok && R >= rmin && R <= rmax;
+    return ok ? v : make_double2(0.0, 0.0);
+  };
+
+  // windows in march order (behind -> ahead): w1..w5 rows R-4d..R (post-black),
+  // q0..q2 rows R-5d..R-3d (final), fa..fd f of rows R-4d..R-d
+  double2 z = make_double2(0.0, 0.0);
+  double2 w1 = z, w2 = z, w3 = z, w4 = z, w5 = z, q0 = z, q1 = z, q2 = z, fa = z, fb = z, fc = z, fd = z;
+  // prefetch queue: rows R .. R+(PD-1)d of p_in and R-d .. R+(PD-2)d of f in flight
+  double2 np[PD], nf[PD];
+#pragma unroll
+  for (int q = 0; q < PD; ++q) {
+    np[q] = ld(pin, Rbeg + q * DIR);
+    nf[q] = ld(f, Rbeg + (q - 1) * DIR);
+  }
+
+  int R = Rbeg;
+  for (int s = 0; s < nsteps; ++s, R += DIR) {
+    const double2 pR = np[0], fR = nf[0];
+#pragma unroll
+    for (int q = 0; q + 1 < PD; ++q) {
+      np[q] = np[q + 1];
+      nf[q] = nf[q + 1];
+    }
+    np[PD - 1] = ld(pin, R + PD * DIR);
+    nf[PD - 1] = ld(f, R + (PD - 1) * DIR);
+    w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = pR;
+    fa = fb; fb = fc; fc = fd; fd = fR;
+    if (COPY) {  // diagnostic timing build: same traffic, no arithmetic (results are wrong)
+      const int j = R - 4 * DIR;
+      if (out_lane && j >= y0 && j < y1)
+        *reinterpret_cast<double2*>(pout + (size_t)(j - g.row_lo) * P + gi) =
+            make_double2(w1.x + fa.x, w1.y + fa.y);
+      rmaxv = 1.0e300;  // never "converges": fixed sweep count for timing
+      continue;
+    }
+    // along the march: "behind" = S for DIR > 0, N for DIR < 0
+#define CFD_S(b, a) ((DIR > 0) ? (b) : (a))
+#define CFD_N(b, a) ((DIR > 0) ? (a) : (b))
+    // red (color 0) at row j = R-d: slot a red iff j even (gi is even)
+    {
+      const int j = R - DIR;
+      const double Lb = dpp_from_left(w4.y), Ra = dpp_from_right(w4.x);
+      const bool rowok = j > rmin && j < rmax;
+      if ((j & 1) == 0) {
+        const double nv = sor_update<CASE>(c, nx, ny, j, gi, w4.x, Lb, w4.y, CFD_S(w3.x, w5.x), CFD_N(w3.x, w5.x), fd.x);
+        w4.x = (rowok && fl_a(j)) ? nv : w4.x;
+      } else {
+        const double nv =
+            sor_update<CASE>(c, nx, ny, j, gi + 1, w4.y, w4.x, Ra, CFD_S(w3.y, w5.y), CFD_N(w3.y, w5.y), fd.y);
+        w4.y = (rowok && fl_b(j)) ? nv : w4.y;
+      }
+    }
+    // black (color 1) at row j = R-2d: slot a black iff j odd
+    {
+      const int j = R - 2 * DIR;
+      const double Lb = dpp_from_left(w3.y), Ra = dpp_from_right(w3.x);
+      const bool rowok = j > rmin && j < rmax;
+      if ((j & 1) == 1) {
+        const double nv = sor_update<CASE>(c, nx, ny, j, gi, w3.x, Lb, w3.y, CFD_S(w2.x, w4.x), CFD_N(w2.x, w4.x), fc.x);
+        w3.x = (rowok && fl_a(j)) ? nv : w3.x;
+      } else {
+        const double nv =
+            sor_update<CASE>(c, nx, ny, j, gi + 1, w3.y, w3.x, Ra, CFD_S(w2.y, w4.y), CFD_N(w2.y, w4.y), fc.y);
+        w3.y = (rowok && fl_b(j)) ? nv : w3.y;
+      }
+    }
+    // ghost / solid refresh at row j = R-3d (pre-refresh neighbours)
+    q0 = q1;
+    q1 = q2;
+    q2 = w2;
+    if (CASE != CAVITY) {
+      const int j = R - 3 * DIR;
+      const double Lb = dpp_from_left(w2.y), Ra = dpp_from_right(w2.x);
+      double out;
+      if (refresh_value<CASE>(c, nx, ny, j, gi, w2.x, Lb, w2.y, CFD_S(w1.x, w3.x), CFD_N(w1.x, w3.x), out)) q2.x = out;
+      if (refresh_value<CASE>(c, nx, ny, j, gi + 1, w2.y, w2.x, Ra, CFD_S(w1.y, w3.y), CFD_N(w1.y, w3.y), out))
+        q2.y = out;
+    }
+    // residual + store at row j = R-4d
+    {
+      const int j = R - 4 * DIR;
+      const double Lb = dpp_from_left(q1.y), Ra = dpp_from_right(q1.x);
+      const bool jout = j >= y0 && j < y1;
+      if (out_lane && jout) *reinterpret_cast<double2*>(pout + (size_t)(j - g.row_lo) * P + gi) = q1;
+      const bool jres = jout && j >= g.j0 && j <= g.j1;
+      const double ra = residual_abs<CASE>(c, nx, ny, j, gi, q1.x, Lb, q1.y, CFD_S(q0.x, q2.x), CFD_N(q0.x, q2.x), fa.x);
+      const double rb =
+          residual_abs<CASE>(c, nx, ny, j, gi + 1, q1.y, q1.x, Ra, CFD_S(q0.y, q2.y), CFD_N(q0.y, q2.y), fa.y);
+      rmaxv = fmax(rmaxv, (out_lane && jres && fl_a(j)) ? ra : 0.0);
+      rmaxv = fmax(rmaxv, (out_lane && jres && fl_b(j)) ? rb : 0.0);
+    }
+#undef CFD_S
+#undef CFD_N
+  }
+}
+
+template <int CASE>
+__global__ __launch_bounds__(256) void poisson_wave_kernel(Geo g, Coef c, const double* __restrict__ pin,
+                                                           double* __restrict__ pout, const double* __restrict__ f,
+                                                           PoissonCtl ctl, int k, int TH, int ctiles, int nbands,
+                                                           int flags) {
+  constexpr int H = 4, TWC = 128 - 2 * H;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+
+  // convergence test of the previous iteration, per wave (all waves agree)
+  {
+    const double tol = ctl.tol[0];
+    const bool stopped = ctl.stop[0] != 0;
+    const bool check = (k == 1) || ((k - 1) % ctl.check_every == 0);
+    bool active;
+    if (stopped) {
+      active = false;
+    } else if (!check) {
+      active = true;
+    } else {
+      double prev;
+      if (k == 1) {
+        prev = ctl.tol[1];
+      } else {
+        const double* slot = ctl.ring + (size_t)((k - 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+        prev = (lane < RES_SHARDS) ? slot[lane * SHARD_STRIDE] : 0.0;
+        prev = wave_max(prev);
+      }
+      active = prev > tol;
+      if (!active && lane == 0 && wv == 0 && blockIdx.x == 0) {
+        ctl.stop[1] = k - 1;
+        ctl.stop[0] = 1;
+      }
+    }
+    if (!active) return;
+  }
+  if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS)
+    ctl.ring[(size_t)((k + 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
+
+  // XCD-aware block order; the 4 waves of a block take 4 adjacent bands
+  const int nblk = (int)gridDim.x;
+  const int L8 = (nblk / 8) * 8;
+  const int bl = (int)blockIdx.x;
+  const int blk = ((flags & 2) && bl < L8) ? (bl % 8) * (nblk / 8) + bl / 8 : bl;
+  const int tile = blk * 4 + wv;
+  if (tile >= ctiles * nbands) return;
+  const int band = tile % nbands, ctile = tile / nbands;
+  const int gi = ctile * TWC - H + 2 * lane;  // this lane's columns: gi (slot a), gi+1 (slot b)
+  const int y0 = g.wj0 + band * TH;
+  const int y1 = min(y0 + TH, g.wj1 + 1);
+  if (y0 > g.wj1) return;
+  double rmaxv = 0.0;
+  const bool up = (flags & 1) && (band & 1);
+  if (CASE == CAVITY && (flags & 8)) {  // diagnostic: traffic only
+    if (up) wave_march<CASE, -1, 4, true>(g, c, pin, pout, f, lane, gi, y0, y1, rmaxv);
+    else wave_march<CASE, 1, 4, true>(g, c, pin, pout, f, lane, gi, y0, y1, rmaxv);
+  } else {
+    if (up) wave_march<CASE, -1, 4>(g, c, pin, pout, f, lane, gi, y0, y1, rmaxv);
+    else wave_march<CASE, 1, 4>(g, c, pin, pout, f, lane, gi, y0, y1, rmaxv);
+  }
+  rmaxv = wave_max(rmaxv);
+  if (lane == 0) {
+    double* slot = ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+    atomicMax(reinterpret_cast<unsigned long long*>(slot + (size_t)(tile % RES_SHARDS) * SHARD_STRIDE),
+              (unsigned long long)__double_as_longlong(rmaxv));
+  }
 }
 
 // ------------------------------------------------------------ corrector --

@@ -10,6 +10,7 @@
 // device (halo copies on the stream) or one per rank (halo rows over RCCL).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -35,7 +36,8 @@ static void check_launch(const char* what) {
 
 enum { B_P0 = 0, B_P1, B_F, B_US, B_VS, B_U, B_V, B_UC, B_VC, NB };
 
-constexpr int PBX = 64, PBY = 32;  // Poisson tile
+constexpr int PBX = 64, PBY = 32;  // Poisson tile (fused-tile variant)
+constexpr int MARCH_MIN_TH = 24;   // minimum rows per band (column-march variant)
 
 struct Strip {
   Geo g{};
@@ -60,6 +62,8 @@ static Coef make_coef(const cfd_params& p) {
   c.rho = p.rho;
   c.u_ref = p.u_ref;
   c.omega = p.omega;
+  c.one_m_omega = 1.0 - p.omega;
+  for (int n = 0; n < 5; ++n) c.om_nc[n] = (n > 0) ? p.omega / n : 0.0;
   c.h2 = p.dx * p.dx;
   c.denom = 2.0 * (c.idx2 + c.idy2);
   c.cav_src = (1.0 / p.dt) * p.rho;
@@ -92,18 +96,38 @@ class Solver {
   double* h_shard = nullptr;  // pinned: RES_SHARDS*SHARD_STRIDE
   hipEvent_t ev_poll[2] = {}, ev_a = nullptr, ev_b = nullptr;
   cfd_timing T{};
+  int kernel_variant = 0;  // 0: wave march (default), 1: fused LDS tile, 2: block column march
+  int resident_waves = 2048;  // wave-march tiles in flight (CUs x 4 SIMDs x waves per SIMD)
+  int resident_blocks = 1024;  // march-kernel blocks resident at once on this device
+  int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order
+  int march_min_th = MARCH_MIN_TH;
 
   Solver(const cfd_params& p, int device, const std::vector<std::pair<int, int>>& rows, Comm* cm)
       : P(p), dev(device), comm(cm) {
     validate();
     C = make_coef(P);
+    if (const char* kv = std::getenv("CFD_POISSON_KERNEL")) {
+      const std::string v(kv);
+      kernel_variant = (v == "tile") ? 1 : (v == "march") ? 2 : 0;
+    }
     HIPC(hipSetDevice(dev));
     hipDeviceProp_t prop;
     HIPC(hipGetDeviceProperties(&prop, dev));
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
       throw Error(CFD_E_DEVICE, std::string("libcfd_amd requires gfx950 (MI355X); device is ") + prop.gcnArchName);
     HIPC(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    pitch = ((P.nx + 2) + 15) / 16 * 16;
+    {
+      int per_cu = 0;
+      HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, poisson_march_kernel<CAVITY>, 256, 0));
+      if (const char* e = std::getenv("CFD_MARCH_BLOCKS_PER_CU")) per_cu = std::atoi(e);
+      resident_blocks = std::max(1, per_cu) * prop.multiProcessorCount;
+      if (const char* e = std::getenv("CFD_MARCH_FLAGS")) march_flags = std::atoi(e);
+      int wps = 4;
+      if (const char* e = std::getenv("CFD_WAVE_WPS")) wps = std::max(1, std::atoi(e));
+      resident_waves = wps * 4 * prop.multiProcessorCount;
+      if (const char* e = std::getenv("CFD_MARCH_MIN_TH")) march_min_th = std::max(8, std::atoi(e));
+    }
+    pitch = ((P.nx + 3) + 15) / 16 * 16;  // >= nx+3: column pairs (gi, gi+1) stay inside a row
     size_t part = 0;
     for (auto [j0, j1] : rows) {
       Strip s;
@@ -294,10 +318,34 @@ class Solver {
     PoissonCtl ctl{ring, tolv, stop, P.check_every};
     for (size_t q = 0; q < S.size(); ++q) {
       const Geo& g = S[q].g;
-      const dim3 grid((P.nx + 2 + PBX - 1) / PBX, (g.wj1 - g.wj0 + 1 + PBY - 1) / PBY);
-      poisson_rbsor_kernel<CASE, PBX, PBY><<<grid, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k);
+      const int rows = g.wj1 - g.wj0 + 1;
+      if (kernel_variant == 1) {
+        const dim3 grid((P.nx + 2 + PBX - 1) / PBX, (rows + PBY - 1) / PBY);
+        poisson_rbsor_kernel<CASE, PBX, PBY><<<grid, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k);
+      } else if (kernel_variant == 2) {
+        constexpr int TW = 256 - 8;
+        // one resident round: split each column tile's rows evenly over the
+        // blocks the device holds at once (no tail of a second, partial round)
+        const int ctiles = (P.nx + 2 + TW - 1) / TW;
+        const int per_tile = std::max(1, resident_blocks / (ctiles * (int)S.size()));
+        const int bands = std::max(1, std::min(per_tile, (rows + march_min_th - 1) / march_min_th));
+        const int th = (rows + bands - 1) / bands;
+        const int nbands = (rows + th - 1) / th;
+        poisson_march_kernel<CASE><<<ctiles * nbands, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k, th,
+                                                                    ctiles, nbands, march_flags);
+      } else {
+        constexpr int TWC = 128 - 8;
+        const int ctiles = (P.nx + 2 + TWC - 1) / TWC;
+        const int per_tile = std::max(1, resident_waves / (ctiles * (int)S.size()));
+        const int bands = std::max(1, std::min(per_tile, (rows + march_min_th - 1) / march_min_th));
+        const int th = (rows + bands - 1) / bands;
+        const int nbands = (rows + th - 1) / th;
+        const int nblk = (ctiles * nbands + 3) / 4;
+        poisson_wave_kernel<CASE><<<nblk, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k, th, ctiles,
+                                                         nbands, march_flags);
+      }
     }
-    check_launch("poisson_rbsor");
+    check_launch("poisson");
   }
 
   void poisson_iteration(int k, int base) {
