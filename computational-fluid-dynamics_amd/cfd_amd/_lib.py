@@ -33,8 +33,11 @@ class CfdParams(ctypes.Structure):
         ("print_interval", ctypes.c_int), ("save_interval", ctypes.c_int),
         ("h_inlet", ctypes.c_double), ("step_x", ctypes.c_double),
         ("step_i", ctypes.c_int), ("inlet_jmax", ctypes.c_int),
-        ("check_every", ctypes.c_int), ("chunk", ctypes.c_int),
+        ("check_every", ctypes.c_int), ("chunk", ctypes.c_int), ("ordering", ctypes.c_int),
     ]
+
+
+ORDER = {"rb": 0, "lex": 1}
 
 
 class StepInfo(ctypes.Structure):

@@ -983,6 +983,206 @@ __global__ __launch_bounds__(256) void poisson_wave_kernel(Geo g, Coef c, const 
   }
 }
 
+// Sequential sums in the reference's loop order (j outer, i inner, fluid cells),
+// for the bit-identical (lexicographic) mode: mode 0 = sum of the source
+// (channel-01.cpp:622-624), mode 1 = kinetic energy 0.5*(u_c^2+v_c^2)
+// (cavity-01.cpp:750-755). One thread; used at reference sizes only.
+__global__ void seq_sum_kernel(Geo g, Coef c, const double* __restrict__ a, const double* __restrict__ b, int mode,
+                               double* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int j = max(g.j0, 1); j <= min(g.j1, g.ny); ++j)
+    for (int i = 1; i <= g.nx; ++i) {
+      if (!is_fluid(c, g.nx, g.ny, j, i)) continue;
+      const size_t o = at(g, j, i);
+      if (mode == 0) s += a[o];
+      else s += 0.5 * (a[o] * a[o] + b[o] * b[o]);
+    }
+  out[0] = s;
+}
+
+// ------------------------------------------- Poisson, exact lexicographic --
+//
+// The reference's own SOR ordering (Gauss-Seidel sweep in j-then-i order,
+// ghosts/solids refreshed after each sweep, residual after the refresh —
+// cavity-01.cpp:635-678, channel-01.cpp:652-682, backwards_step-01.cpp:893-931),
+// reproduced bit for bit on the GPU as a pipelined wavefront:
+//   * cell (j,i) at iteration k is computed at step tau = i + j + 3k; its W/S
+//     inputs (iteration k) were computed at tau-1, its E/N/self inputs
+//     (iteration k-1) at tau-2 / tau-3; iteration k is stored in X[k & 1];
+//   * ghost / solid neighbours are evaluated from stored iteration-(k-1)
+//     values with the reference's refresh rules (all their inputs lie within
+//     distance 2, computed by tau-1);
+//   * in the same step each cell also evaluates the residual of its own
+//     iteration k-1 (all inputs complete by tau-1 and not yet overwritten);
+//   * iteration k's max-norm residual is complete once the last diagonal has
+//     passed; the first k with residual <= tol ends the solve — cells near the
+//     origin have run ahead by then, so the solve restores its initial field
+//     and replays exactly k iterations (no convergence test on the replay).
+// One persistent workgroup runs the whole solve (reference-sized grids).
+
+constexpr int LEX_WIN = 4096;  // residual window (iterations in flight)
+
+template <int CASE>
+__device__ __forceinline__ double lex_value(const Coef& c, int nx, int ny, const Geo& g, const double* X, int j, int i,
+                                            double self_old, bool from_self) {
+  // value of cell (j,i) at the iteration stored in X, as the SOR sweep sees it:
+  // interior fluid -> stored; ghost -> refresh rule; solid -> average of fluid
+  // neighbours (backwards_step-01.cpp:708-738); cavity ghosts are stored zeros.
+  if (CASE == CAVITY) return X[at(g, j, i)];
+  const bool jin = j >= 1 && j <= ny, iin = i >= 1 && i <= nx;
+  if (jin && iin) {
+    if (CASE != BACKSTEP || is_fluid(c, nx, ny, j, i)) return X[at(g, j, i)];
+    double sum = 0.0;
+    int n = 0;
+    if (i > 1 && is_fluid(c, nx, ny, j, i - 1)) { sum += X[at(g, j, i - 1)]; n++; }
+    if (i < nx && is_fluid(c, nx, ny, j, i + 1)) { sum += X[at(g, j, i + 1)]; n++; }
+    if (j > 1 && is_fluid(c, nx, ny, j - 1, i)) { sum += X[at(g, j - 1, i)]; n++; }
+    if (j < ny && is_fluid(c, nx, ny, j + 1, i)) { sum += X[at(g, j + 1, i)]; n++; }
+    return n > 0 ? sum / n : X[at(g, j, i)];
+  }
+  // ghost adjacent to a fluid cell: mirrors that cell (or 0 at the outlet)
+  if (i == nx + 1 && jin) return 0.0;
+  (void)from_self;
+  return self_old;
+}
+
+template <int CASE>
+__global__ __launch_bounds__(1024) void poisson_lex_kernel(Geo g, Coef c, double* __restrict__ X0,
+                                                           double* __restrict__ X1, const double* __restrict__ p0,
+                                                           const double* __restrict__ f, const double* __restrict__ tolv,
+                                                           int max_iters, int* __restrict__ out_iters,
+                                                           double* __restrict__ out_res) {
+  __shared__ double win[LEX_WIN];
+  __shared__ int s_stop, s_kmax, s_replay;
+  const int t = threadIdx.x, NT = blockDim.x;
+  const int nx = g.nx, ny = g.ny;
+  const double tol = tolv[0];
+  const int ncell = nx * ny;
+  const int dmax = nx + ny;  // largest i + j
+  for (int q = t; q < LEX_WIN; q += NT) win[q] = 0.0;
+  if (t == 0) {
+    s_stop = 0;
+    s_replay = 0;
+    s_kmax = max_iters;
+  }
+  __syncthreads();
+  if (!(tolv[1] > tol) || max_iters == 0) {  // loop never entered (cavity-01.cpp:635)
+    if (t == 0) { *out_iters = 0; *out_res = tolv[1]; }
+    return;
+  }
+  int tau = 0;
+  for (;;) {
+    const int kmax = s_kmax;
+    const bool replay = s_replay != 0;
+    // one wavefront step
+    for (int e = t; e < ncell; e += NT) {
+      const int jj = e / nx, j = jj + 1, i = e - jj * nx + 1;
+      const int r = tau - i - j;
+      if (r < 3 || r % 3 != 0) continue;
+      const int k = r / 3;  // this step: residual of k-1, update to k
+      if (k - 1 > kmax) continue;
+      if (!is_fluid(c, nx, ny, j, i)) continue;
+      const double* Xo = ((k - 1) & 1) ? X1 : X0;  // iteration k-1
+      double* Xn = (k & 1) ? X1 : X0;              // iteration k
+      const double self = Xo[at(g, j, i)];
+      const double fc = f[at(g, j, i)];
+      const double oE = lex_value<CASE>(c, nx, ny, g, Xo, j, i + 1, self, true);
+      const double oN = lex_value<CASE>(c, nx, ny, g, Xo, j + 1, i, self, true);
+      const double oW = lex_value<CASE>(c, nx, ny, g, Xo, j, i - 1, self, true);
+      const double oS = lex_value<CASE>(c, nx, ny, g, Xo, j - 1, i, self, true);
+      if (k >= 2 && !replay) {
+        const double rv = fabs(residual_at<CASE>(c, nx, ny, j, i, self, oW, oE, oS, oN, fc));
+        atomicMax(reinterpret_cast<unsigned long long*>(&win[(k - 1) % LEX_WIN]),
+                  (unsigned long long)__double_as_longlong(rv));
+      }
+      if (k <= kmax) {
+        // W/S: iteration k if interior fluid (already swept), else the refreshed value of k-1
+        const bool wf = is_fluid(c, nx, ny, j, i - 1), sf = is_fluid(c, nx, ny, j - 1, i);
+        const double pW = wf ? Xn[at(g, j, i - 1)] : oW;
+        const double pS = sf ? Xn[at(g, j - 1, i)] : oS;
+        Xn[at(g, j, i)] = sor_update<CASE>(c, nx, ny, j, i, self, pW, oE, pS, oN, fc);
+      }
+    }
+    __syncthreads();
+    // iteration kc's residual is complete after the step with tau = dmax + 3(kc+1)
+    if (t == 0) {
+      const int r = tau - dmax;
+      if (r >= 6 && r % 3 == 0) {
+        const int kc = r / 3 - 1;
+        if (replay) {
+          if (kc >= kmax) s_stop = 1;
+        } else {
+          const double rk = win[kc % LEX_WIN];
+          win[kc % LEX_WIN] = 0.0;  // slot reused by iteration kc + LEX_WIN
+          if (!(rk > tol) || kc >= max_iters) {
+            *out_iters = kc;
+            *out_res = rk;
+            if (kc < max_iters && tau - 3 * kc > 3) {
+              // converged at kc while later iterations already ran: replay exactly kc
+              s_replay = 1;
+              s_kmax = kc;
+            } else {
+              s_stop = 1;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (s_stop) break;
+    if (s_replay && !replay) {  // restore the solve's initial field and restart the wavefront
+      for (int e = t; e < (int)((size_t)g.nrows * g.pitch); e += NT) X0[e] = p0[e];
+      __syncthreads();
+      tau = 0;
+      continue;
+    }
+    ++tau;
+  }
+  // refresh ghosts / solids of the final field from its interior (reference order:
+  // walls read pre-refresh solids, so compute everything first, then write)
+  if (CASE != CAVITY) {
+    const int K = *out_iters;
+    double* Xf = (K & 1) ? X1 : X0;
+    const double* Xp = (K & 1) ? X0 : X1;  // iteration K-1
+    const int W2 = nx + 2, n2 = (ny + 2) * (nx + 2);
+    __syncthreads();
+    if (CASE == BACKSTEP && K >= 2) {
+      // solid cells as the sweep of iteration K left them: refreshed from iteration K-1
+      for (int e = t; e < n2; e += NT) {
+        const int j = e / W2, i = e - j * W2;
+        if (j >= 1 && j <= ny && i >= 1 && i <= nx && !is_fluid(c, nx, ny, j, i))
+          Xf[at(g, j, i)] = lex_value<CASE>(c, nx, ny, g, Xp, j, i, 0.0, false);
+      }
+      __syncthreads();
+    }
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int e = t; e < n2; e += NT) {
+        const int j = e / W2, i = e - j * W2;
+        const bool jin = j >= 1 && j <= ny, iin = i >= 1 && i <= nx;
+        double v;
+        bool set = true;
+        if (i == 0 && jin) v = Xf[at(g, j, 1)];
+        else if (i == nx + 1 && jin) v = 0.0;
+        else if (j == 0 && iin) v = Xf[at(g, 1, i)];
+        else if (j == ny + 1 && iin) v = Xf[at(g, ny, i)];
+        else set = false;
+        if (pass == 0 && set) Xf[at(g, j, i)] = v;  // walls first: they read interior cells
+        if (pass == 1 && CASE == BACKSTEP && jin && iin && !is_fluid(c, nx, ny, j, i)) {
+          double sum = 0.0;
+          int n = 0;
+          if (i > 1 && is_fluid(c, nx, ny, j, i - 1)) { sum += Xf[at(g, j, i - 1)]; n++; }
+          if (i < nx && is_fluid(c, nx, ny, j, i + 1)) { sum += Xf[at(g, j, i + 1)]; n++; }
+          if (j > 1 && is_fluid(c, nx, ny, j - 1, i)) { sum += Xf[at(g, j - 1, i)]; n++; }
+          if (j < ny && is_fluid(c, nx, ny, j + 1, i)) { sum += Xf[at(g, j + 1, i)]; n++; }
+          if (n > 0) Xf[at(g, j, i)] = sum / n;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // ------------------------------------------------------------ corrector --
 
 // cavity-01.cpp:695-711 / channel-01.cpp:693-702 / backwards_step-01.cpp:944-976.

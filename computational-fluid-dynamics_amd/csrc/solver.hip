@@ -34,7 +34,7 @@ static void check_launch(const char* what) {
   if (e != hipSuccess) throw Error(CFD_E_DEVICE, std::string("launch ") + what + ": " + hipGetErrorString(e));
 }
 
-enum { B_P0 = 0, B_P1, B_F, B_US, B_VS, B_U, B_V, B_UC, B_VC, NB };
+enum { B_P0 = 0, B_P1, B_F, B_US, B_VS, B_U, B_V, B_UC, B_VC, B_PL, NB };  // B_PL: lex-mode initial field
 
 constexpr int PBX = 64, PBY = 32;  // Poisson tile (fused-tile variant)
 constexpr int MARCH_MIN_TH = 24;   // minimum rows per band (column-march variant)
@@ -202,6 +202,11 @@ class Solver {
     if (!(P.omega > 0) || !(P.omega < 2)) throw Error(CFD_E_ARG, "SOR omega must lie in (0, 2)");
     if (P.max_iters < 0) throw Error(CFD_E_ARG, "max_iters must be >= 0");
     if (P.check_every < 1) throw Error(CFD_E_ARG, "check_every must be >= 1");
+    if (P.ordering != CFD_ORDER_RB && P.ordering != CFD_ORDER_LEX) throw Error(CFD_E_ARG, "unknown ordering");
+    if (P.ordering == CFD_ORDER_LEX && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
+      throw Error(CFD_E_ARG, "lexicographic ordering supports nx + ny < 12000");
+    if (P.ordering == CFD_ORDER_LEX && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
+      throw Error(CFD_E_ARG, "lexicographic ordering supports nx + ny < 12000");
     if (P.case_id == CFD_BACKSTEP && (P.step_i <= 0 || P.step_i >= P.nx))
       throw Error(CFD_E_ARG, "Step location is outside computational domain!");
     if (P.case_id == CFD_BACKSTEP && (P.inlet_jmax < 1 || P.inlet_jmax > P.ny))
@@ -291,7 +296,11 @@ class Solver {
       check_launch("source");
     }
     if (P.case_id != CFD_CAVITY) {
-      sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total);
+      if (P.ordering == CFD_ORDER_LEX) {  // the reference's sequential sum, bit for bit
+        seq_sum_kernel<<<1, 64, 0, st>>>(S[0].g, C, S[0].b[B_F], nullptr, 0, total);
+      } else {
+        sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total);
+      }
       check_launch("sum_partials");
       if (comm && comm->nranks > 1) comm_allreduce_sum(comm, total, 1, st);
       for (auto& s : S) {
@@ -369,7 +378,53 @@ class Solver {
 
   // solverPressurePoisson (cavity-01.cpp:609-690, channel-01.cpp:635-688,
   // backwards_step-01.cpp:872-939). Requires build_source() first.
+  // Reference-order SOR (poisson_lex_kernel): one persistent workgroup.
+  void solve_lex(cfd_step_info* out) {
+    if (S.size() != 1 || comm) throw Error(CFD_E_STATE, "lexicographic ordering needs a single-strip solver");
+    Strip& s = S[0];
+    const int base = pcur;
+    const size_t bytes = (size_t)s.g.nrows * pitch * sizeof(double);
+    double* X0 = s.b[base ? B_P1 : B_P0];
+    double* X1 = s.b[base ? B_P0 : B_P1];
+    if (P.case_id == CFD_CAVITY) {  // cavity-01.cpp:610-611: zero field, zero ghosts
+      HIPC(hipMemsetAsync(X0, 0, bytes, st));
+      HIPC(hipMemsetAsync(X1, 0, bytes, st));
+    }
+    solve_tolerance();
+    HIPC(hipMemcpyAsync(s.b[B_PL], X0, bytes, hipMemcpyDeviceToDevice, st));
+    int* d_it = stop;
+    double* d_res = total + 2;
+    HIPC(hipEventRecord(ev_a, st));
+    if (P.case_id == CFD_CAVITY)
+      poisson_lex_kernel<CAVITY><<<1, 1024, 0, st>>>(s.g, C, X0, X1, s.b[B_PL], s.b[B_F], tolv, P.max_iters, d_it, d_res);
+    else if (P.case_id == CFD_CHANNEL)
+      poisson_lex_kernel<CHANNEL><<<1, 1024, 0, st>>>(s.g, C, X0, X1, s.b[B_PL], s.b[B_F], tolv, P.max_iters, d_it, d_res);
+    else
+      poisson_lex_kernel<BACKSTEP><<<1, 1024, 0, st>>>(s.g, C, X0, X1, s.b[B_PL], s.b[B_F], tolv, P.max_iters, d_it, d_res);
+    check_launch("poisson_lex");
+    HIPC(hipEventRecord(ev_b, st));
+    int iters = 0;
+    double res = 0;
+    HIPC(hipMemcpyAsync(&iters, d_it, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(&res, d_res, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
+    T.poisson_ms += ms;
+    T.poisson_launches += 1;
+    T.poisson_cell_updates += (long long)P.nx * P.ny * iters;
+    pcur = (base + iters) & 1;
+    if (out) {
+      out->sor_iterations = iters;
+      out->residual = res;
+    }
+  }
+
   void solve(cfd_step_info* out) {
+    if (P.ordering == CFD_ORDER_LEX) {
+      solve_lex(out);
+      return;
+    }
     const int base = pcur;
     HIPC(hipMemsetAsync(ring, 0, (size_t)RING * RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
     HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
@@ -467,7 +522,10 @@ class Solver {
                                                        partials + s.part_off, divmax);
       check_launch("centers_stats");
     }
-    sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total + 1);
+    if (P.ordering == CFD_ORDER_LEX)
+      seq_sum_kernel<<<1, 64, 0, st>>>(S[0].g, C, S[0].b[B_UC], S[0].b[B_VC], 1, total + 1);
+    else
+      sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total + 1);
     check_launch("sum_partials");
     if (comm && comm->nranks > 1) {
       comm_allreduce_sum(comm, total + 1, 1, st);

@@ -64,7 +64,11 @@ typedef struct cfd_params {
   int step_i, inlet_jmax;  /* derived step indices (backwards_step-01.cpp:386, 493) */
   int check_every;      /* residual test every N SOR iterations (1 = reference) */
   int chunk;            /* SOR launches enqueued between host polls (0 = auto) */
+  int ordering;         /* CFD_ORDER_RB (default, multi-block, strips/ranks) or CFD_ORDER_LEX
+                           (the reference's sweep order, bit-identical; one device, one strip) */
 } cfd_params;
+
+enum cfd_ordering { CFD_ORDER_RB = 0, CFD_ORDER_LEX = 1 };
 
 typedef struct cfd_solver cfd_solver;
 
