@@ -101,17 +101,9 @@ def main() -> int:
     cp = C.make_params("cavity", re=args.re, nx=args.nx, ny=args.ny * world, max_iters=args.max_iters)
     comm = None
     if world > 1:
-        import ctypes
-        buf = (ctypes.c_ubyte * _lib.COMM_ID_BYTES)()
-        if rank == 0:
-            _lib.check(_lib.lib().cfd_comm_unique_id(buf), "cfd_comm_unique_id")
-        obj = [bytes(buf)]
-        dist.broadcast_object_list(obj, src=0)
-        buf = (ctypes.c_ubyte * _lib.COMM_ID_BYTES).from_buffer_copy(obj[0])
-        comm = _lib.lib().cfd_comm_init(buf, world, rank, local_rank)
-        if not comm:
-            raise _lib.CfdError("cfd_comm_init: " + _lib.lib().cfd_last_error().decode())
-        rows = (rank * args.ny + 1, (rank + 1) * args.ny)
+        from cfd_amd.dist import init_comm, weak_rows
+        comm = init_comm(dist, rank, world, local_rank)
+        rows = weak_rows(rank, args.ny)
         solver = C.CavitySolver(cp, device=local_rank, check_every=check_every, rank_rows=rows, comm=comm)
     else:
         solver = C.CavitySolver(cp, device=local_rank, check_every=check_every)
@@ -141,12 +133,9 @@ def main() -> int:
 
     updates = float(tm.poisson_cell_updates)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        u = torch.tensor([updates], dtype=torch.float64)
-        dist.all_reduce(u, op=dist.ReduceOp.SUM)
-        updates = float(u.item())
+        from cfd_amd.dist import max_over_ranks, sum_over_ranks
+        elapsed = max_over_ranks(dist, elapsed)
+        updates = sum_over_ranks(dist, updates)
 
     if rank == 0:
         g0, g1 = solver.owned_rows()
