@@ -3,6 +3,7 @@
 
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "../../include/cfd_amd.h"
 
@@ -17,16 +18,33 @@ void set_last_error(const std::string& msg);
 
 // RCCL transport (comm.cpp). Loaded with dlopen on first use so the
 // single-GPU library has no RCCL dependency.
+struct LoopHub;  // in-process transport (testing the rank path on one device)
+struct LoopOp {
+  int kind;  // 0 send, 1 recv
+  double* buf;
+  size_t count;
+  int peer;
+};
+
 struct Comm {
   void* nccl = nullptr;  // ncclComm_t
   int nranks = 1, rank = 0, device = 0;
+  LoopHub* hub = nullptr;  // non-null: loopback transport instead of RCCL
+  std::vector<LoopOp> pending;
+  void* ev_ready = nullptr;  // hipEvent_t (loopback)
+  void* ev_done = nullptr;
+  double* tmp = nullptr;     // loopback all-reduce scratch
+  size_t tmp_count = 0;
 };
 
 void comm_unique_id(unsigned char* id_out);
 Comm* comm_init(const unsigned char* id, int nranks, int rank, int device);
+LoopHub* loop_hub_create(int nranks);
+void loop_hub_destroy(LoopHub* h);
+Comm* comm_init_loopback(LoopHub* h, int rank, int device);
 void comm_destroy(Comm* c);
-void comm_group_start();
-void comm_group_end();
+void comm_group_start(Comm* c);
+void comm_group_end(Comm* c, void* stream);
 void comm_send(Comm* c, const double* buf, size_t count, int peer, void* stream);
 void comm_recv(Comm* c, double* buf, size_t count, int peer, void* stream);
 void comm_allreduce_max(Comm* c, double* buf, size_t count, void* stream);

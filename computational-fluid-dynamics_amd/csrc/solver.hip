@@ -237,7 +237,7 @@ class Solver {
       double* base = s.b[b];
       const size_t cnt = (size_t)depth * pitch;
       auto row = [&](int j) { return base + (size_t)(j - g.row_lo) * pitch; };
-      comm_group_start();
+      comm_group_start(comm);
       if (comm->rank > 0) {
         comm_send(comm, row(g.j0), cnt, comm->rank - 1, st);
         comm_recv(comm, row(g.j0 - depth), cnt, comm->rank - 1, st);
@@ -246,7 +246,7 @@ class Solver {
         comm_send(comm, row(g.j1 - depth + 1), cnt, comm->rank + 1, st);
         comm_recv(comm, row(g.j1 + 1), cnt, comm->rank + 1, st);
       }
-      comm_group_end();
+      comm_group_end(comm, st);
     }
   }
 
@@ -778,5 +778,21 @@ void* cfd_comm_init(const unsigned char* id, int nranks, int rank, int device) {
 }
 
 int cfd_comm_destroy(void* comm) { return guard([&] { cfd::comm_destroy(static_cast<cfd::Comm*>(comm)); }); }
+
+void* cfd_comm_loopback_hub(int nranks) {
+  void* out = nullptr;
+  guard([&] { out = cfd::loop_hub_create(nranks); });
+  return out;
+}
+
+void* cfd_comm_init_loopback(void* hub, int rank, int device) {
+  void* out = nullptr;
+  guard([&] { out = cfd::comm_init_loopback(static_cast<cfd::LoopHub*>(hub), rank, device); });
+  return out;
+}
+
+int cfd_comm_loopback_hub_destroy(void* hub) {
+  return guard([&] { cfd::loop_hub_destroy(static_cast<cfd::LoopHub*>(hub)); });
+}
 
 }  // extern "C"

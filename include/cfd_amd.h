@@ -158,6 +158,13 @@ int cfd_comm_unique_id(unsigned char* id_out);
 void* cfd_comm_init(const unsigned char* id, int nranks, int rank, int device);
 int cfd_comm_destroy(void* comm);
 
+/* In-process transport with the same semantics, for ranks that share one
+ * device and run in separate host threads of one process (RCCL refuses two
+ * ranks on one GPU): exercises the rank code path without RCCL. */
+void* cfd_comm_loopback_hub(int nranks);
+void* cfd_comm_init_loopback(void* hub, int rank, int device);
+int cfd_comm_loopback_hub_destroy(void* hub);
+
 #ifdef __cplusplus
 }
 #endif

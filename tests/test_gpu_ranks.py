@@ -1,0 +1,102 @@
+"""The multi-process (rank) code path on one GPU: ranks run in host threads of
+one process and exchange halos / all-reduce through the library's in-process
+loopback transport (RCCL refuses two ranks on one device). Everything but the
+RCCL calls themselves is the code the 8-GPU run executes: rank strips, halo
+row indices, the residual all-reduce feeding each rank's convergence test,
+the source-sum and stats reductions, rank-local field transfer."""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import cfd_amd as C  # noqa: E402
+from cfd_amd import _lib  # noqa: E402
+from cfd_amd.dist import strip_rows  # noqa: E402
+
+
+def run_ranks(cp, world, steps, check_every=1):
+    L = _lib.lib()
+    hub = L.cfd_comm_loopback_hub(world)
+    assert hub
+    results = [None] * world
+    errors = []
+
+    def body(r):
+        try:
+            comm = L.cfd_comm_init_loopback(hub, r, 0)
+            assert comm, L.cfd_last_error()
+            s = C.solver_for(cp, rank_rows=strip_rows(r, world, cp.ny), comm=comm, check_every=check_every)
+            if cp.case_id == C.CAVITY:
+                s.applyBoundaryConditions()
+            its = [s.step() for _ in range(steps)]
+            md, ke = s.statistics()
+            results[r] = dict(rows=s.owned_rows(), u=s.field("u"), v=s.field("v"), p=s.field("p"), its=its,
+                              stats=(md, ke))
+            s.close()
+            L.cfd_comm_destroy(comm)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    L.cfd_comm_loopback_hub_destroy(hub)
+    assert not errors, errors
+    return results
+
+
+def single(cp, steps):
+    s = C.solver_for(cp)
+    if cp.case_id == C.CAVITY:
+        s.applyBoundaryConditions()
+    its = [s.step() for _ in range(steps)]
+    return s, its
+
+
+@pytest.mark.parametrize("case,world,steps", [("cavity", 2, 15), ("cavity", 3, 10), ("channel", 2, 10),
+                                               ("backwards_step", 2, 2)])
+def test_rank_path_equals_single_domain(case, world, steps):
+    cp = C.reference_defaults(case)
+    res = run_ranks(cp, world, steps)
+    s, its = single(cp, steps)
+    ref = {n: s.field(n) for n in ("u", "v", "p")}
+    for r in res:
+        if case == "cavity":
+            assert r["its"] == its
+        else:
+            assert [i for i, _ in r["its"]] == [i for i, _ in its]
+        j0, j1 = r["rows"]
+        first = 0 if j0 == 1 else j0
+        for n in ("u", "v", "p"):
+            rows_total = ref[n].shape[0]
+            last = min(j1 + 1 if j1 == cp.ny else j1, rows_total - 1)
+            a, b = r[n], ref[n][first:last + 1]
+            if case == "cavity":
+                assert np.array_equal(a.view(np.int64), b.view(np.int64)), (n, r["rows"])
+            else:
+                np.testing.assert_allclose(a, b, rtol=0, atol=1e-9 * max(np.abs(b).max(), 1.0))
+    md, ke = s.statistics()
+    for r in res:
+        if case == "cavity":
+            assert r["stats"][0] == md
+        else:  # source mean summed per rank then all-reduced: re-associated
+            assert r["stats"][0] == pytest.approx(md, rel=1e-9)
+        assert r["stats"][1] == pytest.approx(ke, rel=1e-12)
+
+
+def test_rank_path_check_every_8():
+    """The multi-GPU default tests the residual every 8 sweeps: it may run up to 7
+    sweeps past the reference's stopping point, never fewer, and still converges."""
+    cp = C.reference_defaults("cavity")
+    res = run_ranks(cp, 2, 5, check_every=8)
+    _, its = single(cp, 5)
+    for r in res:
+        for (ig, rg), (i1, _r1) in zip(r["its"], its):
+            assert i1 <= ig <= i1 + 7
+            assert ig % 8 == 0 or ig == cp.max_iters
