@@ -29,6 +29,7 @@ struct Options {
   double re = 0, dt = 0, final_time = 0;
   int nx = 0, ny = 0, steps = -1, max_iters = 0, save = 0, print = 0, device = 0, strips = 1, check_every = 1;
   bool vtk = true;
+  bool exact = false;
   std::string outdir = "vtk_output";
 };
 
@@ -36,7 +37,8 @@ inline void usage(const char* prog) {
   std::cerr << "usage: " << prog
             << " [--Re R] [--Nx N] [--Ny N] [--dt DT] [--final-time T] [--steps K] [--max-iters N]\n"
                "       [--save-interval N] [--print-interval N] [--output-dir DIR] [--no-vtk]\n"
-               "       [--device D] [--strips S] [--check-every C]\n";
+               "       [--device D] [--strips S] [--check-every C] [--exact]\n"
+               "  --exact: the reference's lexicographic SOR order (bit-identical output, one strip)\n";
 }
 
 inline Options parse(int argc, char** argv) {
@@ -61,6 +63,7 @@ inline Options parse(int argc, char** argv) {
     else if (a == "--print-interval") o.print = std::atoi(next());
     else if (a == "--output-dir") o.outdir = next();
     else if (a == "--no-vtk") o.vtk = false;
+    else if (a == "--exact") o.exact = true;
     else if (a == "--device") o.device = std::atoi(next());
     else if (a == "--strips") o.strips = std::atoi(next());
     else if (a == "--check-every") o.check_every = std::atoi(next());
@@ -99,6 +102,7 @@ inline int run_case(int case_id, int argc, char** argv) {
   if (o.save > 0) p.save_interval = o.save;
   if (o.print > 0) p.print_interval = o.print;
   p.check_every = o.check_every;
+  if (o.exact) p.ordering = CFD_ORDER_LEX;
   const int total = o.steps >= 0 ? o.steps : p.total_steps;
   const char* base = case_id == CFD_CAVITY ? "cavity_flow" : case_id == CFD_CHANNEL ? "channel_flow" : "backwards_step";
   const std::string coll = std::string(base) + (case_id == CFD_BACKSTEP ? "_animation.pvd" : "_animation.pvd");
