@@ -19,6 +19,9 @@
 namespace cfd {
 
 constexpr int CAVITY = 0, CHANNEL = 1, BACKSTEP = 2;
+#ifndef CFD_WAVE_MIN_WAVES
+#define CFD_WAVE_MIN_WAVES 3  // waves per SIMD the SOR wave kernel must fit (4 would cap VGPRs at 128 and spill)
+#endif
 constexpr int HALO = 4;           // halo rows stored per side (Poisson needs 4)
 constexpr int RES_SHARDS = 32;    // residual / max accumulators, one 128-B line each
 constexpr int SHARD_STRIDE = 16;  // doubles between shards (128 B)
@@ -916,8 +919,174 @@ __device__ __forceinline__ void wave_march(const Geo& g, const Coef& c, const do
   }
 }
 
+// Ring-window version of wave_march (the default): every window is a 5-slot
+// ring addressed with compile-time slots and the march is unrolled by 5, so
+// rows never move between registers (the shifting version spends ~50 moves
+// per row). Slot of the row x*d behind the front row R at rotation ROT:
+#define CFD_SLOT(X) ((((ROT) + 4 - (X)) % 5 + 10) % 5)
+
+struct WaveRing {
+  double2 w[5];   // post-black values, rows R-4d .. R
+  double2 q[5];   // final values, rows R-5d .. R-3d
+  double2 fr[5];  // source, rows R-d .. R-4d
+  double2 np[5];  // prefetched p_in rows R .. R+4d
+  double2 nf[5];  // prefetched f rows R-d .. R+3d
+  double rmax;
+};
+
 template <int CASE>
-__global__ __launch_bounds__(256) void poisson_wave_kernel(Geo g, Coef c, const double* __restrict__ pin,
+struct WaveCtx {
+  Geo g;
+  const Coef& c;  // stays in kernel-argument memory (om_nc is indexed at run time)
+  const double* pin;
+  double* pout;
+  const double* f;
+  int gi, gic, y0, y1, rmin, rmax;
+  bool pair_ok, out_lane, icol_a, icol_b, open_a, open_b;
+  __device__ bool fl_a(int j) const { return icol_a && j >= 1 && j <= g.ny && (open_a || j <= c.inlet_jmax); }
+  __device__ bool fl_b(int j) const { return icol_b && j >= 1 && j <= g.ny && (open_b || j <= c.inlet_jmax); }
+  __device__ double2 ld(const double* base, int R) const {
+    const int Rc = min(max(R, rmin), rmax);
+    const double2 v = *reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * (size_t)g.pitch + gic);
+    return (pair_ok && R >= rmin && R <= rmax) ? v : make_double2(0.0, 0.0);
+  }
+};
+
+template <int CASE, int DIR, int ROT>
+__device__ __forceinline__ void wave_ring_step(const WaveCtx<CASE>& x, WaveRing& s, int R) {
+  const int nx = x.g.nx, ny = x.g.ny;
+  const Coef& c = x.c;
+  // consume the prefetched row R (and f row R-d); issue the loads 4 rows ahead
+  s.w[CFD_SLOT(0)] = s.np[CFD_SLOT(0)];
+  s.fr[CFD_SLOT(1)] = s.nf[CFD_SLOT(0)];
+  s.np[CFD_SLOT(-4)] = x.ld(x.pin, R + 4 * DIR);
+  s.nf[CFD_SLOT(-4)] = x.ld(x.f, R + 3 * DIR);
+#define CFD_S(b, a) ((DIR > 0) ? (b) : (a))
+#define CFD_N(b, a) ((DIR > 0) ? (a) : (b))
+  // red (color 0) at row j = R-d: slot a is red iff j is even
+  {
+    const int j = R - DIR;
+    double2& m = s.w[CFD_SLOT(1)];
+    const double2 bh = s.w[CFD_SLOT(2)], ah = s.w[CFD_SLOT(0)];
+    const double2 fc = s.fr[CFD_SLOT(1)];
+    const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
+    const bool rowok = j > x.rmin && j < x.rmax;
+    if ((j & 1) == 0) {
+      const double nv = sor_update<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+      m.x = (rowok && x.fl_a(j)) ? nv : m.x;
+    } else {
+      const double nv =
+          sor_update<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+      m.y = (rowok && x.fl_b(j)) ? nv : m.y;
+    }
+  }
+  // black (color 1) at row j = R-2d
+  {
+    const int j = R - 2 * DIR;
+    double2& m = s.w[CFD_SLOT(2)];
+    const double2 bh = s.w[CFD_SLOT(3)], ah = s.w[CFD_SLOT(1)];
+    const double2 fc = s.fr[CFD_SLOT(2)];
+    const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
+    const bool rowok = j > x.rmin && j < x.rmax;
+    if ((j & 1) == 1) {
+      const double nv = sor_update<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+      m.x = (rowok && x.fl_a(j)) ? nv : m.x;
+    } else {
+      const double nv =
+          sor_update<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+      m.y = (rowok && x.fl_b(j)) ? nv : m.y;
+    }
+  }
+  // ghost / solid refresh at row j = R-3d (pre-refresh neighbours) -> q
+  {
+    const double2 m = s.w[CFD_SLOT(3)];
+    double2 nv = m;
+    if (CASE != CAVITY) {
+      const int j = R - 3 * DIR;
+      const double2 bh = s.w[CFD_SLOT(4)], ah = s.w[CFD_SLOT(2)];
+      const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
+      double out;
+      if (refresh_value<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), out)) nv.x = out;
+      if (refresh_value<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), out))
+        nv.y = out;
+    }
+    s.q[CFD_SLOT(3)] = nv;
+  }
+  // residual + store at row j = R-4d: q rows R-5d (behind), R-4d, R-3d (ahead)
+  {
+    const int j = R - 4 * DIR;
+    const double2 m = s.q[CFD_SLOT(4)], bh = s.q[CFD_SLOT(5)], ah = s.q[CFD_SLOT(3)];
+    const double2 fc = s.fr[CFD_SLOT(4)];
+    const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
+    const bool jout = j >= x.y0 && j < x.y1;
+    if (x.out_lane && jout)
+      *reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi) = m;
+    const bool jres = x.out_lane && jout && j >= x.g.j0 && j <= x.g.j1;
+    const double ra = residual_abs<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+    const double rb =
+        residual_abs<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+    s.rmax = fmax(s.rmax, (jres && x.fl_a(j)) ? ra : 0.0);
+    s.rmax = fmax(s.rmax, (jres && x.fl_b(j)) ? rb : 0.0);
+  }
+#undef CFD_S
+#undef CFD_N
+}
+
+template <int CASE, int DIR>
+__device__ __forceinline__ double wave_march_ring(const Geo& g, const Coef& c, const double* __restrict__ pin,
+                                                  double* __restrict__ pout, const double* __restrict__ f, int lane,
+                                                  int gi, int y0, int y1) {
+  constexpr int H = 4;
+  WaveCtx<CASE> x{g, c};
+  x.pin = pin; x.pout = pout; x.f = f;
+  x.gi = gi;
+  x.y0 = y0;
+  x.y1 = y1;
+  x.rmin = max(g.row_lo, 0);
+  x.rmax = min(g.row_lo + g.nrows - 1, g.ny + 1);
+  x.pair_ok = gi >= 0 && gi + 1 < g.pitch;
+  x.out_lane = x.pair_ok && lane >= H / 2 && lane < 64 - H / 2;
+  x.icol_a = gi >= 1 && gi <= g.nx;
+  x.icol_b = gi + 1 >= 1 && gi + 1 <= g.nx;
+  x.open_a = (CASE != BACKSTEP) || (gi > c.step_i);
+  x.open_b = (CASE != BACKSTEP) || (gi + 1 > c.step_i);
+  x.gic = min(max(gi, 0), g.pitch - 2);
+  const int Rbeg = (DIR > 0) ? y0 - H : y1 - 1 + H;
+  const int nsteps = (y1 - y0) + 2 * H;
+  WaveRing s;
+  const double2 z = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) s.w[k] = s.q[k] = s.fr[k] = z;
+  s.rmax = 0.0;
+  {
+    constexpr int ROT = 0;  // slots as seen by the first step
+    s.np[CFD_SLOT(0)] = x.ld(pin, Rbeg);
+    s.np[CFD_SLOT(-1)] = x.ld(pin, Rbeg + DIR);
+    s.np[CFD_SLOT(-2)] = x.ld(pin, Rbeg + 2 * DIR);
+    s.np[CFD_SLOT(-3)] = x.ld(pin, Rbeg + 3 * DIR);
+    s.nf[CFD_SLOT(0)] = x.ld(f, Rbeg - DIR);
+    s.nf[CFD_SLOT(-1)] = x.ld(f, Rbeg);
+    s.nf[CFD_SLOT(-2)] = x.ld(f, Rbeg + DIR);
+    s.nf[CFD_SLOT(-3)] = x.ld(f, Rbeg + 2 * DIR);
+  }
+  int st = 0, R = Rbeg;
+  for (; st + 5 <= nsteps; st += 5, R += 5 * DIR) {
+    wave_ring_step<CASE, DIR, 0>(x, s, R);
+    wave_ring_step<CASE, DIR, 1>(x, s, R + DIR);
+    wave_ring_step<CASE, DIR, 2>(x, s, R + 2 * DIR);
+    wave_ring_step<CASE, DIR, 3>(x, s, R + 3 * DIR);
+    wave_ring_step<CASE, DIR, 4>(x, s, R + 4 * DIR);
+  }
+  if (st < nsteps) { wave_ring_step<CASE, DIR, 0>(x, s, R); ++st; R += DIR; }
+  if (st < nsteps) { wave_ring_step<CASE, DIR, 1>(x, s, R); ++st; R += DIR; }
+  if (st < nsteps) { wave_ring_step<CASE, DIR, 2>(x, s, R); ++st; R += DIR; }
+  if (st < nsteps) { wave_ring_step<CASE, DIR, 3>(x, s, R); ++st; R += DIR; }
+  return s.rmax;
+}
+#undef CFD_SLOT
+
+template <int CASE>
+__global__ __launch_bounds__(256, CFD_WAVE_MIN_WAVES) void poisson_wave_kernel(Geo g, Coef c, const double* __restrict__ pin,
                                                            double* __restrict__ pout, const double* __restrict__ f,
                                                            PoissonCtl ctl, int k, int TH, int ctiles, int nbands,
                                                            int flags) {
@@ -968,13 +1137,8 @@ __global__ __launch_bounds__(256) void poisson_wave_kernel(Geo g, Coef c, const 
   if (y0 > g.wj1) return;
   double rmaxv = 0.0;
   const bool up = (flags & 1) && (band & 1);
-  if (CASE == CAVITY && (flags & 8)) {  // diagnostic: traffic only
-    if (up) wave_march<CASE, -1, 4, true>(g, c, pin, pout, f, lane, gi, y0, y1, rmaxv);
-    else wave_march<CASE, 1, 4, true>(g, c, pin, pout, f, lane, gi, y0, y1, rmaxv);
-  } else {
-    if (up) wave_march<CASE, -1, 4>(g, c, pin, pout, f, lane, gi, y0, y1, rmaxv);
-    else wave_march<CASE, 1, 4>(g, c, pin, pout, f, lane, gi, y0, y1, rmaxv);
-  }
+  rmaxv = up ? wave_march_ring<CASE, -1>(g, c, pin, pout, f, lane, gi, y0, y1)
+             : wave_march_ring<CASE, 1>(g, c, pin, pout, f, lane, gi, y0, y1);
   rmaxv = wave_max(rmaxv);
   if (lane == 0) {
     double* slot = ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;

@@ -122,7 +122,9 @@ class Solver {
       if (const char* e = std::getenv("CFD_MARCH_BLOCKS_PER_CU")) per_cu = std::atoi(e);
       resident_blocks = std::max(1, per_cu) * prop.multiProcessorCount;
       if (const char* e = std::getenv("CFD_MARCH_FLAGS")) march_flags = std::atoi(e);
-      int wps = 4;
+      int wps = 0;  // waves per SIMD of the wave-march kernel (1 block of 4 waves = 1 wave per SIMD)
+      HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&wps, poisson_wave_kernel<CAVITY>, 256, 0));
+      wps = std::max(1, std::min(wps, 4));
       if (const char* e = std::getenv("CFD_WAVE_WPS")) wps = std::max(1, std::atoi(e));
       resident_waves = wps * 4 * prop.multiProcessorCount;
       if (const char* e = std::getenv("CFD_MARCH_MIN_TH")) march_min_th = std::max(8, std::atoi(e));
