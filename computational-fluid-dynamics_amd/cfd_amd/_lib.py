@@ -34,6 +34,7 @@ class CfdParams(ctypes.Structure):
         ("h_inlet", ctypes.c_double), ("step_x", ctypes.c_double),
         ("step_i", ctypes.c_int), ("inlet_jmax", ctypes.c_int),
         ("check_every", ctypes.c_int), ("chunk", ctypes.c_int), ("ordering", ctypes.c_int),
+        ("sweeps_per_launch", ctypes.c_int),
     ]
 
 
@@ -51,7 +52,7 @@ class Stats(ctypes.Structure):
 class Timing(ctypes.Structure):
     _fields_ = [("poisson_ms", ctypes.c_double), ("poisson_launches", ctypes.c_longlong),
                 ("poisson_cell_updates", ctypes.c_longlong), ("step_ms", ctypes.c_double),
-                ("steps", ctypes.c_longlong)]
+                ("steps", ctypes.c_longlong), ("poisson_sweeps", ctypes.c_longlong)]
 
 
 # every symbol include/cfd_amd.h declares: name -> (restype, argtypes)

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import ctypes
 
-HALO = 4  # rows of each neighbour stored per side (csrc/kernels.hpp)
+HALO = 8  # rows of each neighbour stored per side (csrc/kernels.hpp; a fused SOR pair needs 7)
 
 
 def strip_rows(rank: int, world: int, ny_global: int) -> tuple[int, int]:

@@ -19,13 +19,14 @@ from .logfmt import step_line, warning_line
 from .params import BACKSTEP, CASE_NAMES, CAVITY, CHANNEL, CaseParams, make_params
 
 
-def to_cparams(cp: CaseParams, check_every: int = 1, chunk: int = 0, ordering: str = "rb") -> _lib.CfdParams:
+def to_cparams(cp: CaseParams, check_every: int = 1, chunk: int = 0, ordering: str = "rb",
+               sweeps_per_launch: int = 0) -> _lib.CfdParams:
     """Derived reference constants -> the C-ABI parameter block."""
     return _lib.CfdParams(
         cp.case_id, cp.nx, cp.ny, cp.length, cp.height, cp.re, cp.u_ref, cp.rho, cp.cfl, cp.final_time,
         cp.dx, cp.dy, cp.nu, cp.dt, cp.omega, cp.tol_factor, cp.abs_tol, cp.max_iters, cp.total_steps,
         cp.print_interval, cp.save_interval, cp.h_inlet, cp.step_x, cp.step_i, cp.inlet_jmax, check_every, chunk,
-        _lib.ORDER[ordering])
+        _lib.ORDER[ordering], sweeps_per_launch)
 
 
 class _SolverBase:
@@ -35,13 +36,15 @@ class _SolverBase:
 
     def __init__(self, params: CaseParams | None = None, *, device: int = 0, n_strips: int = 1,
                  check_every: int = 1, chunk: int = 0, rank_rows: tuple[int, int] | None = None, comm=None,
-                 ordering: str = "rb"):
+                 ordering: str = "rb", sweeps_per_launch: int = 0):
         """ordering: "rb" (red-black SOR, the fast default) or "lex" (the reference's
-        lexicographic sweep, bit-identical to it; one device, one strip)."""
+        lexicographic sweep, bit-identical to it; one device, one strip).
+        sweeps_per_launch: red-black iterations fused per kernel launch (0 = auto = 2,
+        1 or 2); the result is bit-identical either way."""
         self.params = params if params is not None else make_params(self.CASE)
         if self.params.case_id != self.CASE:
             raise ValueError(f"{type(self).__name__} needs case {CASE_NAMES[self.CASE]}")
-        self._cp = to_cparams(self.params, check_every, chunk, ordering)
+        self._cp = to_cparams(self.params, check_every, chunk, ordering, sweeps_per_launch)
         L = _lib.lib()
         if rank_rows is None:
             self._h = L.cfd_create(ctypes.byref(self._cp), device, n_strips)

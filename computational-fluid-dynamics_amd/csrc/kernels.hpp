@@ -22,10 +22,10 @@ constexpr int CAVITY = 0, CHANNEL = 1, BACKSTEP = 2;
 #ifndef CFD_WAVE_MIN_WAVES
 #define CFD_WAVE_MIN_WAVES 3  // waves per SIMD the SOR wave kernel must fit (4 would cap VGPRs at 128 and spill)
 #endif
-constexpr int HALO = 4;           // halo rows stored per side (Poisson needs 4)
+constexpr int HALO = 8;           // halo rows stored per side (a fused pair of SOR iterations needs 7)
 constexpr int RES_SHARDS = 32;    // residual / max accumulators, one 128-B line each
 constexpr int SHARD_STRIDE = 16;  // doubles between shards (128 B)
-constexpr int RING = 4;           // residual ring slots (iteration k uses k & 3)
+constexpr int RING = 8;           // residual ring slots (iteration k uses k & 7)
 
 struct Geo {
   int nx, ny;      // global interior cells
@@ -368,7 +368,13 @@ __device__ __forceinline__ double sor_update(const Coef& c, int nx, int ny, int 
     const double tE = ee ? pE : copysign(0.0, pE);
     const double tW = ew ? pW : copysign(0.0, pW);
     const double tN = en ? pN : copysign(0.0, pN);
-    return pc * c.one_m_omega + c.om_nc[nc] * ((tE + tW) + (tN + pS) - fc * c.h2);
+    // selected as values: a run-time index into Coef (or a select of its
+    // addresses, which the optimiser forms from a select of loads) copies the
+    // whole struct to scratch; the empty asm keeps the loaded values opaque
+    double o1 = c.om_nc[1], o2 = c.om_nc[2], o3 = c.om_nc[3], o4 = c.om_nc[4];
+    asm("" : "+s"(o1), "+s"(o2), "+s"(o3), "+s"(o4));
+    const double om = (nc == 4) ? o4 : (nc == 3) ? o3 : (nc == 2) ? o2 : o1;
+    return pc * c.one_m_omega + om * ((tE + tW) + (tN + pS) - fc * c.h2);
   } else {
     const double sum = c.idx2 * (pE + pW) + c.idy2 * (pN + pS);
     const double gs = (sum - fc) / c.denom;
@@ -937,7 +943,7 @@ struct WaveRing {
 template <int CASE>
 struct WaveCtx {
   Geo g;
-  const Coef& c;  // stays in kernel-argument memory (om_nc is indexed at run time)
+  const Coef& c;  // kernel-argument memory
   const double* pin;
   double* pout;
   const double* f;
@@ -949,6 +955,11 @@ struct WaveCtx {
     const int Rc = min(max(R, rmin), rmax);
     const double2 v = *reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * (size_t)g.pitch + gic);
     return (pair_ok && R >= rmin && R <= rmax) ? v : make_double2(0.0, 0.0);
+  }
+  // interior waves: every column stored, rows clamped (wave-uniform scalar math)
+  __device__ double2 ld_fast(const double* base, int R) const {
+    const int Rc = min(max(R, rmin), rmax);
+    return *reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * (size_t)g.pitch + gi);
   }
 };
 
@@ -1085,6 +1096,20 @@ __device__ __forceinline__ double wave_march_ring(const Geo& g, const Coef& c, c
 }
 #undef CFD_SLOT
 
+// Convergence test of the residual recorded for iteration kk (launch-start
+// test of the reference's while condition, cavity-01.cpp:633): true = go on.
+__device__ __forceinline__ bool pair_go_on(const PoissonCtl& ctl, int kk, int lane, double tol) {
+  double prev;
+  if (kk == 0) {
+    prev = ctl.tol[1];
+  } else {
+    const double* slot = ctl.ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+    prev = (lane < RES_SHARDS) ? slot[lane * SHARD_STRIDE] : 0.0;
+    prev = wave_max(prev);
+  }
+  return prev > tol;
+}
+
 template <int CASE>
 __global__ __launch_bounds__(256, CFD_WAVE_MIN_WAVES) void poisson_wave_kernel(Geo g, Coef c, const double* __restrict__ pin,
                                                            double* __restrict__ pout, const double* __restrict__ f,
@@ -1093,14 +1118,23 @@ __global__ __launch_bounds__(256, CFD_WAVE_MIN_WAVES) void poisson_wave_kernel(G
   constexpr int H = 4, TWC = 128 - 2 * H;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 
-  // convergence test of the previous iteration, per wave (all waves agree)
-  {
+  // convergence test of the previous iteration, per wave (all waves agree);
+  // flags bit 2 = replay of an iteration already known to be the last one
+  if (!(flags & 4)) {
     const double tol = ctl.tol[0];
     const bool stopped = ctl.stop[0] != 0;
     const bool check = (k == 1) || ((k - 1) % ctl.check_every == 0);
     bool active;
     if (stopped) {
       active = false;
+    } else if ((flags & 8) && k >= 3 && (k - 2) % ctl.check_every == 0 && !pair_go_on(ctl, k - 2, lane, tol)) {
+      // flags bit 3: the previous launch was a pair, whose first iteration
+      // (k-2) no launch has tested yet
+      active = false;
+      if (lane == 0 && wv == 0 && blockIdx.x == 0) {
+        ctl.stop[1] = k - 2;
+        ctl.stop[0] = 1;
+      }
     } else if (!check) {
       active = true;
     } else {
@@ -1144,6 +1178,350 @@ __global__ __launch_bounds__(256, CFD_WAVE_MIN_WAVES) void poisson_wave_kernel(G
     double* slot = ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
     atomicMax(reinterpret_cast<unsigned long long*>(slot + (size_t)(tile % RES_SHARDS) * SHARD_STRIDE),
               (unsigned long long)__double_as_longlong(rmaxv));
+  }
+}
+
+// ------------------------------------- Poisson, two iterations per launch --
+//
+// Temporal blocking of the wave march: one launch runs SOR iterations k and
+// k+1. Iteration k's pipeline is the one above (red at R-1, black at R-2,
+// refresh at R-3, residual at R-4; no store); its final rows feed a second
+// pipeline, lagging 3 rows (red at R-4, black at R-5, refresh at R-6, residual
+// + store at R-7). Every cell sees the same operands in the same order as in
+// two single-iteration launches, so the result is bit-identical; the launch
+// reads p and f once and writes p once (24 B/cell) for two iterations.
+// Dependency depth: 7 rows / columns, so a wave writes 112 of its 128 columns
+// (8-column halos) and bands overlap by 7 rows. Both residuals are recorded
+// (ring slots k and k+1); if iteration k alone meets the tolerance the host
+// replays it with one single-iteration launch from this launch's input.
+
+constexpr int PAIR_H = 7;                     // row / column dependency depth of a pair
+constexpr int PAIR_TWC = 128 - 2 * 8;         // output columns per wave (8-column halos)
+
+#define CFD_SLOT(X) ((((ROT) + 4 - (X)) % 5 + 10) % 5)
+
+struct WavePair {
+  double2 w[5];   // iteration k, post-black rows R-4d .. R
+  double2 q[5];   // iteration k, final rows R-5d .. R-3d
+  double2 w2[5];  // iteration k+1, post-black rows R-7d .. R-3d
+  double2 q2[5];  // iteration k+1, final rows R-8d .. R-6d
+  double2 fr[5];  // source rows R-d .. R-5d
+  double2 fr2[5]; // source rows R-6d .. R-10d
+  double2 np[5];  // prefetched p_in rows R .. R+4d
+  double2 nf[5];  // prefetched f rows R-d .. R+3d
+  double rmax1, rmax2;
+};
+
+// Interior SOR update / residual magnitude: every neighbour is a fluid cell
+// (cavity: all four indicators are 1, so the reference's products are the
+// plain values). Same operations in the same order as sor_update /
+// residual_abs, hence the same bits; no selects.
+template <int CASE>
+__device__ __forceinline__ double sor_interior(const Coef& c, double pc, double pW, double pE, double pS, double pN,
+                                               double fc) {
+  if (CASE == CAVITY) return pc * c.one_m_omega + c.om_nc[4] * ((pE + pW) + (pN + pS) - fc * c.h2);
+  const double sum = c.idx2 * (pE + pW) + c.idy2 * (pN + pS);
+  const double gs = (sum - fc) / c.denom;
+  return c.one_m_omega * pc + c.omega * gs;
+}
+template <int CASE>
+__device__ __forceinline__ double residual_interior(const Coef& c, double pc, double pW, double pE, double pS,
+                                                    double pN, double fc) {
+  if (CASE == CAVITY) return fabs(c.idx2 * ((pE - pc) + (pW - pc) + (pN - pc) + (pS - pc)) - fc);
+  const double lap = (pE - 2.0 * pc + pW) * c.idx2 + (pN - 2.0 * pc + pS) * c.idy2;
+  return fabs(lap - fc);
+}
+
+// One pipeline stage set of one iteration on ring rows: red at A-d, black at
+// A-2d, refresh at A-3d into Q, residual (+ store) at A-4d, where row A-xd of
+// W sits in slot CFD_SLOT(x + OFF). FAST: the wave's cells and their
+// dependency cone are interior fluid cells of rows that are updated (checked
+// per wave by the caller), so no per-cell masks are evaluated; the residual
+// of halo lanes is masked once at the end instead of per row.
+template <int CASE, int DIR, int ROT, int OFF, bool FAST, int APAR>
+__device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)[5], double2 (&Q)[5],
+                                            const double2& f_red, const double2& f_black, const double2& f_res,
+                                            int A, bool store, double& rm) {
+  const int nx = x.g.nx, ny = x.g.ny;
+  const Coef& c = x.c;
+#define CFD_S(b, a) ((DIR > 0) ? (b) : (a))
+#define CFD_N(b, a) ((DIR > 0) ? (a) : (b))
+  {  // red (color 0) at row A-d
+    const int j = A - DIR;  // parity APAR ^ 1 (compile time)
+    double2& m = W[CFD_SLOT(1 + OFF)];
+    const double2 bh = W[CFD_SLOT(2 + OFF)], ah = W[CFD_SLOT(0 + OFF)];
+    if ((APAR == 2) ? ((j & 1) == 0) : ((APAR ^ 1) == 0)) {  // APAR 2: parity known at run time only
+      const double Lb = dpp_from_left(m.y);
+      if (FAST) {
+        m.x = sor_interior<CASE>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
+      } else {
+        const double nv =
+            sor_update<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
+        m.x = (j > x.rmin && j < x.rmax && x.fl_a(j)) ? nv : m.x;
+      }
+    } else {
+      const double Ra = dpp_from_right(m.x);
+      if (FAST) {
+        m.y = sor_interior<CASE>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
+      } else {
+        const double nv =
+            sor_update<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
+        m.y = (j > x.rmin && j < x.rmax && x.fl_b(j)) ? nv : m.y;
+      }
+    }
+  }
+  {  // black (color 1) at row A-2d
+    const int j = A - 2 * DIR;  // parity APAR
+    double2& m = W[CFD_SLOT(2 + OFF)];
+    const double2 bh = W[CFD_SLOT(3 + OFF)], ah = W[CFD_SLOT(1 + OFF)];
+    if ((APAR == 2) ? ((j & 1) == 1) : (APAR == 1)) {
+      const double Lb = dpp_from_left(m.y);
+      if (FAST) {
+        m.x = sor_interior<CASE>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
+      } else {
+        const double nv =
+            sor_update<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
+        m.x = (j > x.rmin && j < x.rmax && x.fl_a(j)) ? nv : m.x;
+      }
+    } else {
+      const double Ra = dpp_from_right(m.x);
+      if (FAST) {
+        m.y = sor_interior<CASE>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
+      } else {
+        const double nv =
+            sor_update<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
+        m.y = (j > x.rmin && j < x.rmax && x.fl_b(j)) ? nv : m.y;
+      }
+    }
+  }
+  {  // ghost / solid refresh at row A-3d (pre-refresh neighbours) -> Q; none for interior fluid cells
+    const double2 m = W[CFD_SLOT(3 + OFF)];
+    double2 nv = m;
+    if (CASE != CAVITY && !FAST) {
+      const int j = A - 3 * DIR;
+      const double2 bh = W[CFD_SLOT(4 + OFF)], ah = W[CFD_SLOT(2 + OFF)];
+      const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
+      double out;
+      if (refresh_value<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), out)) nv.x = out;
+      if (refresh_value<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), out))
+        nv.y = out;
+    }
+    Q[CFD_SLOT(3 + OFF)] = nv;
+  }
+  {  // residual (+ store) at row A-4d: Q rows A-5d (behind), A-4d, A-3d (ahead)
+    const int j = A - 4 * DIR;
+    const bool jout = j >= x.y0 && j < x.y1;  // wave-uniform
+    if (jout) {
+      const double2 m = Q[CFD_SLOT(4 + OFF)], bh = Q[CFD_SLOT(5 + OFF)], ah = Q[CFD_SLOT(3 + OFF)];
+      const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
+      if (store && x.out_lane)
+        *reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi) = m;
+      if (FAST) {
+        rm = fmax(rm, residual_interior<CASE>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x));
+        rm = fmax(rm, residual_interior<CASE>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_res.y));
+      } else if (j >= x.g.j0 && j <= x.g.j1) {
+        const double ra =
+            residual_abs<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x);
+        const double rb =
+            residual_abs<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_res.y);
+        rm = fmax(rm, (x.out_lane && x.fl_a(j)) ? ra : 0.0);
+        rm = fmax(rm, (x.out_lane && x.fl_b(j)) ? rb : 0.0);
+      }
+    }
+  }
+#undef CFD_S
+#undef CFD_N
+}
+
+template <int CASE, int DIR, int ROT, bool FAST, int PAR>  // PAR = parity of R (2: not known at compile time)
+__device__ __forceinline__ void wave_pair_step(const WaveCtx<CASE>& x, WavePair& s, int R) {
+  // consume the prefetched row R (and f row R-d); issue the loads 4 rows ahead
+  s.fr2[CFD_SLOT(6)] = s.fr[CFD_SLOT(6)];  // f row R-6d leaves fr (its slot takes row R-d) for fr2
+  s.w[CFD_SLOT(0)] = s.np[CFD_SLOT(0)];
+  s.fr[CFD_SLOT(1)] = s.nf[CFD_SLOT(0)];
+  if (FAST) {  // rows clamped to stored memory (wave-uniform); out-of-range rows are never consumed
+    s.np[CFD_SLOT(-4)] = x.ld_fast(x.pin, R + 4 * DIR);
+    s.nf[CFD_SLOT(-4)] = x.ld_fast(x.f, R + 3 * DIR);
+  } else {
+    s.np[CFD_SLOT(-4)] = x.ld(x.pin, R + 4 * DIR);
+    s.nf[CFD_SLOT(-4)] = x.ld(x.f, R + 3 * DIR);
+  }
+  // iteration k: rows R-d .. R-4d
+  pair_stages<CASE, DIR, ROT, 0, FAST, PAR>(x, s.w, s.q, s.fr[CFD_SLOT(1)], s.fr[CFD_SLOT(2)], s.fr[CFD_SLOT(4)], R, false,
+                                       s.rmax1);
+  // iteration k+1 takes iteration k's newest final row (R-3d) as its front row
+  s.w2[CFD_SLOT(3)] = s.q[CFD_SLOT(3)];
+  pair_stages<CASE, DIR, ROT, 3, FAST, (PAR == 2) ? 2 : (PAR ^ 1)>(x, s.w2, s.q2, s.fr[CFD_SLOT(4)], s.fr[CFD_SLOT(5)], s.fr2[CFD_SLOT(7)],
+                                       R - 3 * DIR, true, s.rmax2);
+}
+
+template <int CASE, int DIR, bool FAST>
+__device__ __forceinline__ void wave_march_pair(const WaveCtx<CASE>& x, int y0, int y1, double& r1, double& r2) {
+  constexpr int H = PAIR_H;
+  // first front row, moved one row outward if needed so that it is even: the
+  // row parity of every stage is then a compile-time constant of the 10-step
+  // unrolled loop (no branches on the red/black colour); the extra leading row
+  // and the trailing rows of the last 10-step group are pipeline fill only
+  // (no store, no residual: outside [y0, y1))
+  const int Rb0 = (DIR > 0) ? y0 - H : y1 - 1 + H;
+  const int Rbeg = Rb0 - DIR * (Rb0 & 1);
+  const int nsteps = (y1 - y0) + 2 * H + (Rb0 & 1);
+  WavePair s;
+  const double2 z = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) s.w[k] = s.q[k] = s.w2[k] = s.q2[k] = s.fr[k] = s.fr2[k] = z;
+  s.rmax1 = s.rmax2 = 0.0;
+  {
+    constexpr int ROT = 0;  // slots as seen by the first step
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s.np[CFD_SLOT(-q)] = FAST ? x.ld_fast(x.pin, Rbeg + q * DIR) : x.ld(x.pin, Rbeg + q * DIR);
+      s.nf[CFD_SLOT(-q)] = FAST ? x.ld_fast(x.f, Rbeg + (q - 1) * DIR) : x.ld(x.f, Rbeg + (q - 1) * DIR);
+    }
+  }
+  int R = Rbeg;
+  for (int st = 0; st < nsteps; st += 10, R += 10 * DIR) {
+    wave_pair_step<CASE, DIR, 0, FAST, 0>(x, s, R);
+    wave_pair_step<CASE, DIR, 1, FAST, 1>(x, s, R + DIR);
+    wave_pair_step<CASE, DIR, 2, FAST, 0>(x, s, R + 2 * DIR);
+    wave_pair_step<CASE, DIR, 3, FAST, 1>(x, s, R + 3 * DIR);
+    wave_pair_step<CASE, DIR, 4, FAST, 0>(x, s, R + 4 * DIR);
+    wave_pair_step<CASE, DIR, 0, FAST, 1>(x, s, R + 5 * DIR);
+    wave_pair_step<CASE, DIR, 1, FAST, 0>(x, s, R + 6 * DIR);
+    wave_pair_step<CASE, DIR, 2, FAST, 1>(x, s, R + 7 * DIR);
+    wave_pair_step<CASE, DIR, 3, FAST, 0>(x, s, R + 8 * DIR);
+    wave_pair_step<CASE, DIR, 4, FAST, 1>(x, s, R + 9 * DIR);
+  }
+  r1 = FAST ? (x.out_lane ? s.rmax1 : 0.0) : s.rmax1;
+  r2 = FAST ? (x.out_lane ? s.rmax2 : 0.0) : s.rmax2;
+}
+
+// Boundary waves (ghost / solid cells in the cone): general masks, one march
+// direction and a 5-step unroll with the colour tested at run time - compact
+// code, so that it shares the instruction cache with the interior loops.
+template <int CASE>
+__device__ __forceinline__ void wave_march_pair_edge(const WaveCtx<CASE>& x, int y0, int y1, double& r1,
+                                                     double& r2) {
+  constexpr int H = PAIR_H, DIR = 1;
+  const int Rbeg = y0 - H;
+  const int nsteps = (y1 - y0) + 2 * H;
+  WavePair s;
+  const double2 z = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) s.w[k] = s.q[k] = s.w2[k] = s.q2[k] = s.fr[k] = s.fr2[k] = z;
+  s.rmax1 = s.rmax2 = 0.0;
+  {
+    constexpr int ROT = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s.np[CFD_SLOT(-q)] = x.ld(x.pin, Rbeg + q * DIR);
+      s.nf[CFD_SLOT(-q)] = x.ld(x.f, Rbeg + (q - 1) * DIR);
+    }
+  }
+  int st = 0, R = Rbeg;
+  for (; st + 5 <= nsteps; st += 5, R += 5) {
+    wave_pair_step<CASE, DIR, 0, false, 2>(x, s, R);
+    wave_pair_step<CASE, DIR, 1, false, 2>(x, s, R + 1);
+    wave_pair_step<CASE, DIR, 2, false, 2>(x, s, R + 2);
+    wave_pair_step<CASE, DIR, 3, false, 2>(x, s, R + 3);
+    wave_pair_step<CASE, DIR, 4, false, 2>(x, s, R + 4);
+  }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 0, false, 2>(x, s, R); ++st; ++R; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 1, false, 2>(x, s, R); ++st; ++R; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 2, false, 2>(x, s, R); ++st; ++R; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 3, false, 2>(x, s, R); ++st; ++R; }
+  r1 = s.rmax1;
+  r2 = s.rmax2;
+}
+#undef CFD_SLOT
+
+#ifndef CFD_PAIR_MIN_WAVES
+#define CFD_PAIR_MIN_WAVES 2
+#endif
+
+template <int CASE>
+__global__ __launch_bounds__(256, CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
+    Geo g, Coef c, const double* __restrict__ pin, double* __restrict__ pout, const double* __restrict__ f,
+    PoissonCtl ctl, int k, int TH, int ctiles, int nbands, int flags) {
+  constexpr int H = 8;  // column halo (lanes 0-3 and 60-63)
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: band / row logic stays scalar
+
+  // convergence tests of iterations k-2 and k-1 (all waves agree): the first
+  // that meets the tolerance (on a checked iteration) ends the solve there
+  {
+    const double tol = ctl.tol[0];
+    if (ctl.stop[0] != 0) return;
+    int stop_at = -1;
+    if (k == 1) {
+      if (!pair_go_on(ctl, 0, lane, tol)) stop_at = 0;
+    } else {
+      const int ka = k - 2, kb = k - 1;
+      if (ka >= 1 && ka % ctl.check_every == 0 && !pair_go_on(ctl, ka, lane, tol)) stop_at = ka;
+      else if (kb % ctl.check_every == 0 && !pair_go_on(ctl, kb, lane, tol)) stop_at = kb;
+    }
+    if (stop_at >= 0) {
+      if (lane == 0 && wv == 0 && blockIdx.x == 0) {
+        ctl.stop[1] = stop_at;
+        ctl.stop[0] = 1;
+      }
+      return;
+    }
+  }
+  if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS) {
+    ctl.ring[(size_t)((k + 2) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
+    ctl.ring[(size_t)((k + 3) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
+  }
+
+  const int nblk = (int)gridDim.x;
+  const int L8 = (nblk / 8) * 8;
+  const int bl = (int)blockIdx.x;
+  const int blk = ((flags & 2) && bl < L8) ? (bl % 8) * (nblk / 8) + bl / 8 : bl;
+  const int tile = blk * 4 + wv;
+  if (tile >= ctiles * nbands) return;
+  const int band = tile % nbands, ctile = tile / nbands;
+  const int gi = ctile * PAIR_TWC - H + 2 * lane;
+  const int y0 = g.wj0 + band * TH;
+  const int y1 = min(y0 + TH, g.wj1 + 1);
+  if (y0 > g.wj1) return;
+  WaveCtx<CASE> x{g, c};
+  x.pin = pin; x.pout = pout; x.f = f;
+  x.gi = gi;
+  x.y0 = y0;
+  x.y1 = y1;
+  x.rmin = max(g.row_lo, 0);
+  x.rmax = min(g.row_lo + g.nrows - 1, g.ny + 1);
+  x.pair_ok = gi >= 0 && gi + 1 < g.pitch;
+  x.out_lane = x.pair_ok && lane >= H / 2 && lane < 64 - H / 2;
+  x.icol_a = gi >= 1 && gi <= g.nx;
+  x.icol_b = gi + 1 >= 1 && gi + 1 <= g.nx;
+  x.open_a = (CASE != BACKSTEP) || (gi > c.step_i);
+  x.open_b = (CASE != BACKSTEP) || (gi + 1 > c.step_i);
+  x.gic = min(max(gi, 0), g.pitch - 2);
+  // interior wave: all 128 columns are fluid cells with fluid neighbours, and
+  // every row of the dependency cone [y0-7, y1+6] is an updated interior row
+  const int c0 = ctile * PAIR_TWC - H;
+  const bool cols_in = c0 >= 1 && c0 + 127 <= g.nx && (CASE != BACKSTEP || c0 > c.step_i + 1);
+  const bool rows_in = y0 - PAIR_H >= max(1, x.rmin + 1) && y1 + PAIR_H - 1 <= min(g.ny, x.rmax - 1);
+  double r1 = 0.0, r2 = 0.0;
+  const bool up = (flags & 1) && (band & 1);
+  // flags bit 4 / bit 5 (timing diagnostics only): never / always take the interior path
+  const bool fast = (flags & 32) || (!(flags & 16) && cols_in && rows_in);
+  if (fast) {
+    if (up) wave_march_pair<CASE, -1, true>(x, y0, y1, r1, r2);
+    else wave_march_pair<CASE, 1, true>(x, y0, y1, r1, r2);
+  } else {
+    wave_march_pair_edge<CASE>(x, y0, y1, r1, r2);
+  }
+  r1 = wave_max(r1);
+  r2 = wave_max(r2);
+  if (lane == 0) {
+    double* s1 = ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+    double* s2 = ctl.ring + (size_t)((k + 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+    atomicMax(reinterpret_cast<unsigned long long*>(s1 + (size_t)(tile % RES_SHARDS) * SHARD_STRIDE),
+              (unsigned long long)__double_as_longlong(r1));
+    atomicMax(reinterpret_cast<unsigned long long*>(s2 + (size_t)(tile % RES_SHARDS) * SHARD_STRIDE),
+              (unsigned long long)__double_as_longlong(r2));
   }
 }
 

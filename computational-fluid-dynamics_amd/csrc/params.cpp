@@ -34,6 +34,7 @@ extern "C" int cfd_params_init(int case_id, double re, int nx, int ny, double dt
   p.check_every = 1;
   p.chunk = 0;
   p.ordering = CFD_ORDER_RB;
+  p.sweeps_per_launch = 0;
   switch (case_id) {
     case CFD_CAVITY:
       p.nx = p.ny = 63; p.length = 1.0; p.height = 1.0; p.re = 1000.0; p.u_ref = 1.0; p.rho = 1.0;

@@ -98,6 +98,7 @@ class Solver {
   cfd_timing T{};
   int kernel_variant = 0;  // 0: wave march (default), 1: fused LDS tile, 2: block column march
   int resident_waves = 2048;  // wave-march tiles in flight (CUs x 4 SIMDs x waves per SIMD)
+  int resident_pair_waves = 2048;  // the same for the two-iteration kernel
   int resident_blocks = 1024;  // march-kernel blocks resident at once on this device
   int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order
   int march_min_th = MARCH_MIN_TH;
@@ -127,6 +128,11 @@ class Solver {
       wps = std::max(1, std::min(wps, 4));
       if (const char* e = std::getenv("CFD_WAVE_WPS")) wps = std::max(1, std::atoi(e));
       resident_waves = wps * 4 * prop.multiProcessorCount;
+      int pps = 0;
+      HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pps, poisson_pair_kernel<CAVITY>, 256, 0));
+      pps = std::max(1, std::min(pps, 4));
+      if (const char* e = std::getenv("CFD_PAIR_WPS")) pps = std::max(1, std::atoi(e));
+      resident_pair_waves = pps * 4 * prop.multiProcessorCount;
       if (const char* e = std::getenv("CFD_MARCH_MIN_TH")) march_min_th = std::max(8, std::atoi(e));
     }
     pitch = ((P.nx + 3) + 15) / 16 * 16;  // >= nx+3: column pairs (gi, gi+1) stay inside a row
@@ -204,6 +210,7 @@ class Solver {
     if (!(P.omega > 0) || !(P.omega < 2)) throw Error(CFD_E_ARG, "SOR omega must lie in (0, 2)");
     if (P.max_iters < 0) throw Error(CFD_E_ARG, "max_iters must be >= 0");
     if (P.check_every < 1) throw Error(CFD_E_ARG, "check_every must be >= 1");
+    if (P.sweeps_per_launch < 0 || P.sweeps_per_launch > 2) throw Error(CFD_E_ARG, "sweeps_per_launch must be 0, 1 or 2");
     if (P.ordering != CFD_ORDER_RB && P.ordering != CFD_ORDER_LEX) throw Error(CFD_E_ARG, "unknown ordering");
     if (P.ordering == CFD_ORDER_LEX && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
       throw Error(CFD_E_ARG, "lexicographic ordering supports nx + ny < 12000");
@@ -324,57 +331,76 @@ class Solver {
     check_launch("tol");
   }
 
+  // Sizing of the wave-march kernels: column tiles of `twc` output columns,
+  // each split into bands so that one resident round covers the strip.
+  void wave_bands(int rows, int twc, int resident, int& ctiles, int& th, int& nbands) const {
+    ctiles = (P.nx + 2 + twc - 1) / twc;
+    const int per_tile = std::max(1, resident / (ctiles * (int)S.size()));
+    const int bands = std::max(1, std::min(per_tile, (rows + march_min_th - 1) / march_min_th));
+    th = (rows + bands - 1) / bands;
+    nbands = (rows + th - 1) / th;
+  }
+
+  // One SOR launch: iteration k (sweeps == 1) or iterations k, k+1 (sweeps == 2).
+  // replay: iteration k is already known to be the solve's last (no test).
   template <int CASE>
-  void launch_poisson(const double* const* pin, double* const* pout, int k) {
+  void launch_poisson(const double* const* pin, double* const* pout, int k, int sweeps, bool replay, bool after_pair) {
     PoissonCtl ctl{ring, tolv, stop, P.check_every};
     for (size_t q = 0; q < S.size(); ++q) {
       const Geo& g = S[q].g;
       const int rows = g.wj1 - g.wj0 + 1;
-      if (kernel_variant == 1) {
+      int ctiles, th, nbands;
+      if (sweeps == 2) {
+        wave_bands(rows, PAIR_TWC, resident_pair_waves, ctiles, th, nbands);
+        // the pair kernel marches in groups of 10 rows over th + 15 rows
+        // (th + 14 + parity alignment): th = 5 mod 10 wastes no group
+        th = std::min(rows, (th + 4) / 10 * 10 + 5);
+        nbands = (rows + th - 1) / th;
+        const int nblk = (ctiles * nbands + 3) / 4;
+        poisson_pair_kernel<CASE><<<nblk, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k, th, ctiles,
+                                                         nbands, march_flags);
+      } else if (kernel_variant == 1 && !replay) {
         const dim3 grid((P.nx + 2 + PBX - 1) / PBX, (rows + PBY - 1) / PBY);
         poisson_rbsor_kernel<CASE, PBX, PBY><<<grid, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k);
-      } else if (kernel_variant == 2) {
+      } else if (kernel_variant == 2 && !replay) {
         constexpr int TW = 256 - 8;
         // one resident round: split each column tile's rows evenly over the
         // blocks the device holds at once (no tail of a second, partial round)
-        const int ctiles = (P.nx + 2 + TW - 1) / TW;
-        const int per_tile = std::max(1, resident_blocks / (ctiles * (int)S.size()));
-        const int bands = std::max(1, std::min(per_tile, (rows + march_min_th - 1) / march_min_th));
-        const int th = (rows + bands - 1) / bands;
-        const int nbands = (rows + th - 1) / th;
+        wave_bands(rows, TW, resident_blocks, ctiles, th, nbands);
         poisson_march_kernel<CASE><<<ctiles * nbands, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k, th,
                                                                     ctiles, nbands, march_flags);
       } else {
-        constexpr int TWC = 128 - 8;
-        const int ctiles = (P.nx + 2 + TWC - 1) / TWC;
-        const int per_tile = std::max(1, resident_waves / (ctiles * (int)S.size()));
-        const int bands = std::max(1, std::min(per_tile, (rows + march_min_th - 1) / march_min_th));
-        const int th = (rows + bands - 1) / bands;
-        const int nbands = (rows + th - 1) / th;
+        wave_bands(rows, 128 - 8, resident_waves, ctiles, th, nbands);
         const int nblk = (ctiles * nbands + 3) / 4;
         poisson_wave_kernel<CASE><<<nblk, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k, th, ctiles,
-                                                         nbands, march_flags);
+                                                         nbands, march_flags | (replay ? 4 : 0) | (after_pair ? 8 : 0));
       }
     }
     check_launch("poisson");
   }
 
-  void poisson_iteration(int k, int base) {
-    const int bin = ((base + k - 1) & 1) ? B_P1 : B_P0;
-    const int bout = ((base + k) & 1) ? B_P1 : B_P0;
-    if (multi()) exchange(bin, HALO);
+  // SOR launch number m (0-based) of a solve starting in buffer `base`: reads
+  // buffer (base+m)&1, writes the other. Iterations k .. k+sweeps-1.
+  void poisson_launch(int m, int k, int sweeps, int base, bool replay = false, bool after_pair = false) {
+    const int bin = ((base + m) & 1) ? B_P1 : B_P0;
+    const int bout = ((base + m + 1) & 1) ? B_P1 : B_P0;
+    if (multi()) exchange(bin, sweeps == 2 ? HALO : 4);
     std::vector<const double*> pin(S.size());
     std::vector<double*> pout(S.size());
     for (size_t q = 0; q < S.size(); ++q) {
       pin[q] = S[q].b[bin];
       pout[q] = S[q].b[bout];
     }
-    if (P.case_id == CFD_CAVITY) launch_poisson<CAVITY>(pin.data(), pout.data(), k);
-    else if (P.case_id == CFD_CHANNEL) launch_poisson<CHANNEL>(pin.data(), pout.data(), k);
-    else launch_poisson<BACKSTEP>(pin.data(), pout.data(), k);
-    if (comm && comm->nranks > 1 && (k % P.check_every == 0 || k == P.max_iters)) {
-      double* slot = ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-      comm_allreduce_max(comm, slot, RES_SHARDS * SHARD_STRIDE, st);
+    if (P.case_id == CFD_CAVITY) launch_poisson<CAVITY>(pin.data(), pout.data(), k, sweeps, replay, after_pair);
+    else if (P.case_id == CFD_CHANNEL) launch_poisson<CHANNEL>(pin.data(), pout.data(), k, sweeps, replay, after_pair);
+    else launch_poisson<BACKSTEP>(pin.data(), pout.data(), k, sweeps, replay, after_pair);
+    if (comm && comm->nranks > 1 && !replay) {
+      for (int kk = k; kk < k + sweeps; ++kk) {
+        if (kk % P.check_every == 0 || kk == P.max_iters) {
+          double* slot = ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+          comm_allreduce_max(comm, slot, RES_SHARDS * SHARD_STRIDE, st);
+        }
+      }
     }
   }
 
@@ -437,14 +463,19 @@ class Solver {
     }
     solve_tolerance();
     if (multi()) exchange(B_F, HALO - 1);
-    const int chunk = P.chunk > 0 ? P.chunk : 32;
+    // Launch plan: pairs of iterations (k, k+1) per launch, a single launch for
+    // an odd last iteration; launch m reads buffer (base+m)&1.
+    const int spl = (P.sweeps_per_launch == 1 || kernel_variant != 0) ? 1 : 2;  // pairs: wave kernels only
+    const int chunk = P.chunk > 0 ? P.chunk : 32;  // launches between host polls
     HIPC(hipEventRecord(ev_a, st));
-    int k = 0, c = 0;
+    int k = 0, c = 0, m = 0;
     bool stopped = false;
     while (k < P.max_iters && !stopped) {
-      const int n = std::min(chunk, P.max_iters - k);
-      for (int j = 1; j <= n; ++j) poisson_iteration(k + j, base);
-      k += n;
+      for (int j = 0; j < chunk && k < P.max_iters; ++j, ++m) {
+        const int n = std::min(spl, P.max_iters - k);
+        poisson_launch(m, k + 1, n, base, false, spl == 2 && k > 0);
+        k += n;
+      }
       HIPC(hipMemcpyAsync(h_stat + 2 * (c & 1), stop, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
       HIPC(hipEventRecord(ev_poll[c & 1], st));
       if (c > 0) {
@@ -465,8 +496,38 @@ class Solver {
     HIPC(hipEventSynchronize(ev_b));
     float ms = 0.f;
     HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
+    // iteration max_iters-1 ran as the first of the last pair: no later launch
+    // tested it, so test it here (the reference's while condition)
+    if (spl == 2 && iters == P.max_iters && P.max_iters >= 2 && P.max_iters % 2 == 0 &&
+        (P.max_iters - 1) % P.check_every == 0) {
+      double t2[2];
+      HIPC(hipMemcpy(t2, tolv, sizeof t2, hipMemcpyDeviceToHost));
+      const double* slot = ring + (size_t)((P.max_iters - 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+      HIPC(hipMemcpy(h_shard, slot, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost));
+      double r = 0.0;
+      for (int q = 0; q < RES_SHARDS; ++q) r = std::max(r, h_shard[q * SHARD_STRIDE]);
+      if (!(r > t2[0])) iters = P.max_iters - 1;
+    }
+    // an odd last iteration that ran as the first of a pair: its pair wrote
+    // iteration iters+1; recompute iteration iters from the pair's input
+    if (spl == 2 && iters > 0 && (iters & 1) && !(iters == P.max_iters && (P.max_iters & 1))) {
+      HIPC(hipEventRecord(ev_a, st));
+      poisson_launch((iters - 1) / 2, iters, 1, base, true);
+      HIPC(hipEventRecord(ev_b, st));
+      HIPC(hipEventSynchronize(ev_b));
+      float ms2 = 0.f;
+      HIPC(hipEventElapsedTime(&ms2, ev_a, ev_b));
+      ms += ms2;
+    }
+    // launches that did work (later ones in the enqueued chunks exit at entry)
+    long long work_launches = (iters + spl - 1) / spl, work_sweeps = iters;
+    if (spl == 2 && (iters & 1) && !(iters == P.max_iters && (P.max_iters & 1))) {
+      work_launches += 1;  // the replay
+      work_sweeps += 2;    // the pair computed iteration iters+1, the replay redid iters
+    }
     T.poisson_ms += ms;
-    T.poisson_launches += k;
+    T.poisson_launches += work_launches;
+    T.poisson_sweeps += work_sweeps;
     long long owned = 0;
     for (auto& s : S) owned += (long long)(s.g.j1 - s.g.j0 + 1) * P.nx;
     T.poisson_cell_updates += owned * iters;
@@ -481,7 +542,10 @@ class Solver {
       res = 0.0;
       for (int q = 0; q < RES_SHARDS; ++q) res = std::max(res, h_shard[q * SHARD_STRIDE]);
     }
-    pcur = (base + iters) & 1;
+    // launch m's output is buffer (base+m+1)&1; iteration `iters` was written by
+    // launch ceil(iters/spl)-1 (or its replay, into the same buffer)
+    const int last_launch = (iters + spl - 1) / spl;
+    pcur = (base + last_launch) & 1;
     if (out) {
       out->sor_iterations = iters;
       out->residual = res;
@@ -651,7 +715,7 @@ cfd_solver* cfd_create(const cfd_params* p, int device, int n_strips) {
   guard([&] {
     if (!p) throw Error(CFD_E_ARG, "null params");
     if (n_strips < 1) throw Error(CFD_E_ARG, "n_strips must be >= 1");
-    if (p->ny < n_strips * cfd::HALO) throw Error(CFD_E_ARG, "each strip needs at least 4 rows");
+    if (p->ny < n_strips * cfd::HALO) throw Error(CFD_E_ARG, "each strip needs at least 8 rows (the SOR halo depth)");
     std::vector<std::pair<int, int>> rows;
     for (int k = 0; k < n_strips; ++k) {
       const int a = 1 + (int)((long long)p->ny * k / n_strips);

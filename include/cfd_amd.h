@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 1
+#define CFD_AMD_ABI_VERSION 2
 
 enum cfd_case { CFD_CAVITY = 0, CFD_CHANNEL = 1, CFD_BACKSTEP = 2 };
 
@@ -66,6 +66,8 @@ typedef struct cfd_params {
   int chunk;            /* SOR launches enqueued between host polls (0 = auto) */
   int ordering;         /* CFD_ORDER_RB (default, multi-block, strips/ranks) or CFD_ORDER_LEX
                            (the reference's sweep order, bit-identical; one device, one strip) */
+  int sweeps_per_launch; /* red-black SOR iterations fused into one kernel launch: 0 = auto (2),
+                           1 or 2; results are bit-identical either way */
 } cfd_params;
 
 enum cfd_ordering { CFD_ORDER_RB = 0, CFD_ORDER_LEX = 1 };
@@ -88,6 +90,7 @@ typedef struct cfd_timing {
   long long poisson_cell_updates; /* interior cells x active iterations (this rank) */
   double step_ms;             /* device time of whole timesteps */
   long long steps;
+  long long poisson_sweeps;   /* SOR iterations executed by those launches (2 per fused launch) */
 } cfd_timing;
 
 /* Library / ABI info. */

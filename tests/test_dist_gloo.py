@@ -3,9 +3,11 @@
 The GPU data path (RCCL send/recv of halo rows inside libcfd_amd.so) needs
 GPUs; here we check the host logic around it and the decomposition itself:
 row partitioning, RCCL-id bootstrap over a process group, max-over-ranks
-timing, and a numpy emulation of the fused red-black SOR iteration on two
-strips exchanging HALO=4 rows over gloo — it must equal the single-domain
-iteration bit for bit (the property the GPU kernels rely on: redundant
+timing, and a numpy emulation of the fused red-black SOR launches on two
+strips: HALO=8 rows exchanged over gloo, then two iterations computed locally
+(the GPU's two-iteration kernel, poisson_pair_kernel), a single one for an odd
+last iteration. It must equal the single-domain iteration bit for bit, both
+residuals included (the property the GPU kernels rely on: redundant
 recomputation of the halo rows reproduces the neighbour's arithmetic).
 """
 from __future__ import annotations
@@ -92,7 +94,9 @@ def _worker(rank, world, port, q, nx, ny, iters):
         f = np.zeros((len(rows), nx + 2)); f[valid] = f_full[rows[valid]]
         p = np.zeros_like(f)
         res_hist = []
-        for _ in range(iters):
+        done = 0
+        while done < iters:
+            n = min(2, iters - done)  # iterations fused into this launch
             # exchange HALO owned rows with the neighbours (the GPU path: ncclSend/ncclRecv)
             if rank > 0:
                 dist.send(torch.from_numpy(p[HALO:2 * HALO].copy()), rank - 1)
@@ -103,9 +107,12 @@ def _worker(rank, world, port, q, nx, ny, iters):
                 top = p[-2 * HALO:-HALO].copy()
                 dist.send(torch.from_numpy(top), rank + 1)
                 p[-HALO:] = buf.numpy()
-            pn = rb_iteration(p, f, nx, ny, omega, h, lo, None)
-            r = residual(pn, f, nx, ny, h, lo)[HALO:-HALO].max()
-            res_hist.append(max_over_ranks(dist, r))
+            pn = p
+            for _ in range(n):  # halo rows recomputed redundantly, no exchange in between
+                pn = rb_iteration(pn, f, nx, ny, omega, h, lo, None)
+                r = residual(pn, f, nx, ny, h, lo)[HALO:-HALO].max()
+                res_hist.append(max_over_ranks(dist, r))
+            done += n
             # keep owned rows (halo rows are refreshed by the next exchange)
             p[HALO:-HALO] = pn[HALO:-HALO]
             if rank == 0:
