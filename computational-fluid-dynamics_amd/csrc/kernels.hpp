@@ -1232,6 +1232,24 @@ __device__ __forceinline__ double residual_interior(const Coef& c, double pc, do
   return fabs(lap - fc);
 }
 
+template <int CASE>
+struct WaveCtx;
+
+// SOR update of an interior-column cell on an updated row j (row-uniform):
+// cavity rows below the top have four neighbours; the top row (j == ny) has
+// eps_n = 0 and its north neighbour is the ghost row, which holds +0.0, so the
+// reference's 0*p[ny+1][i] equals p[ny+1][i] and only omega/3 differs.
+template <int CASE>
+__device__ __forceinline__ double sor_fast(const WaveCtx<CASE>& x, int j, double pc, double pW, double pE, double pS,
+                                           double pN, double fc) {
+  const Coef& c = x.c;
+  if (CASE == CAVITY) {
+    const double om = (j == x.g.ny) ? c.om_nc[3] : c.om_nc[4];  // row-uniform: a scalar select
+    return pc * c.one_m_omega + om * ((pE + pW) + (pN + pS) - fc * c.h2);
+  }
+  return sor_interior<CASE>(c, pc, pW, pE, pS, pN, fc);
+}
+
 // One pipeline stage set of one iteration on ring rows: red at A-d, black at
 // A-2d, refresh at A-3d into Q, residual (+ store) at A-4d, where row A-xd of
 // W sits in slot CFD_SLOT(x + OFF). FAST: the wave's cells and their
@@ -1253,7 +1271,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     if ((APAR == 2) ? ((j & 1) == 0) : ((APAR ^ 1) == 0)) {  // APAR 2: parity known at run time only
       const double Lb = dpp_from_left(m.y);
       if (FAST) {
-        m.x = sor_interior<CASE>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
+        if (j > x.rmin && j < x.rmax) m.x = sor_fast<CASE>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
@@ -1262,7 +1280,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     } else {
       const double Ra = dpp_from_right(m.x);
       if (FAST) {
-        m.y = sor_interior<CASE>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
+        if (j > x.rmin && j < x.rmax) m.y = sor_fast<CASE>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
@@ -1277,7 +1295,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     if ((APAR == 2) ? ((j & 1) == 1) : (APAR == 1)) {
       const double Lb = dpp_from_left(m.y);
       if (FAST) {
-        m.x = sor_interior<CASE>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
+        if (j > x.rmin && j < x.rmax) m.x = sor_fast<CASE>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
@@ -1286,7 +1304,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     } else {
       const double Ra = dpp_from_right(m.x);
       if (FAST) {
-        m.y = sor_interior<CASE>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
+        if (j > x.rmin && j < x.rmax) m.y = sor_fast<CASE>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
@@ -1297,6 +1315,11 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
   {  // ghost / solid refresh at row A-3d (pre-refresh neighbours) -> Q; none for interior fluid cells
     const double2 m = W[CFD_SLOT(3 + OFF)];
     double2 nv = m;
+    if (CASE != CAVITY && FAST) {  // interior columns: only the ghost rows refresh (row-uniform)
+      const int j = A - 3 * DIR;
+      if (j == 0) nv = CFD_N(W[CFD_SLOT(4 + OFF)], W[CFD_SLOT(2 + OFF)]);       // p[0][i] = p[1][i]
+      if (j == ny + 1) nv = CFD_S(W[CFD_SLOT(4 + OFF)], W[CFD_SLOT(2 + OFF)]);  // p[ny+1][i] = p[ny][i]
+    }
     if (CASE != CAVITY && !FAST) {
       const int j = A - 3 * DIR;
       const double2 bh = W[CFD_SLOT(4 + OFF)], ah = W[CFD_SLOT(2 + OFF)];
@@ -1317,8 +1340,15 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
       if (store && x.out_lane)
         *reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi) = m;
       if (FAST) {
-        rm = fmax(rm, residual_interior<CASE>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x));
-        rm = fmax(rm, residual_interior<CASE>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_res.y));
+        if (j >= x.g.j0 && j <= x.g.j1) {  // row-uniform
+          if (CASE == CAVITY && j == ny) {  // top row: eps_n = 0 (cavity-01.cpp:666)
+            rm = fmax(rm, residual_abs<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x));
+            rm = fmax(rm, residual_abs<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_res.y));
+          } else {
+            rm = fmax(rm, residual_interior<CASE>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x));
+            rm = fmax(rm, residual_interior<CASE>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_res.y));
+          }
+        }
       } else if (j >= x.g.j0 && j <= x.g.j1) {
         const double ra =
             residual_abs<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x);
@@ -1396,14 +1426,14 @@ __device__ __forceinline__ void wave_march_pair(const WaveCtx<CASE>& x, int y0, 
   r2 = FAST ? (x.out_lane ? s.rmax2 : 0.0) : s.rmax2;
 }
 
-// Boundary waves (ghost / solid cells in the cone): general masks, one march
-// direction and a 5-step unroll with the colour tested at run time - compact
-// code, so that it shares the instruction cache with the interior loops.
-template <int CASE>
+// Boundary-column waves (ghost / solid columns in the tile): general masks
+// and a 5-step unroll with the colour tested at run time - compact code, so
+// that it shares the instruction cache with the interior loops.
+template <int CASE, int DIR>
 __device__ __forceinline__ void wave_march_pair_edge(const WaveCtx<CASE>& x, int y0, int y1, double& r1,
                                                      double& r2) {
-  constexpr int H = PAIR_H, DIR = 1;
-  const int Rbeg = y0 - H;
+  constexpr int H = PAIR_H;
+  const int Rbeg = (DIR > 0) ? y0 - H : y1 - 1 + H;
   const int nsteps = (y1 - y0) + 2 * H;
   WavePair s;
   const double2 z = make_double2(0.0, 0.0);
@@ -1419,17 +1449,17 @@ __device__ __forceinline__ void wave_march_pair_edge(const WaveCtx<CASE>& x, int
     }
   }
   int st = 0, R = Rbeg;
-  for (; st + 5 <= nsteps; st += 5, R += 5) {
+  for (; st + 5 <= nsteps; st += 5, R += 5 * DIR) {
     wave_pair_step<CASE, DIR, 0, false, 2>(x, s, R);
-    wave_pair_step<CASE, DIR, 1, false, 2>(x, s, R + 1);
-    wave_pair_step<CASE, DIR, 2, false, 2>(x, s, R + 2);
-    wave_pair_step<CASE, DIR, 3, false, 2>(x, s, R + 3);
-    wave_pair_step<CASE, DIR, 4, false, 2>(x, s, R + 4);
+    wave_pair_step<CASE, DIR, 1, false, 2>(x, s, R + DIR);
+    wave_pair_step<CASE, DIR, 2, false, 2>(x, s, R + 2 * DIR);
+    wave_pair_step<CASE, DIR, 3, false, 2>(x, s, R + 3 * DIR);
+    wave_pair_step<CASE, DIR, 4, false, 2>(x, s, R + 4 * DIR);
   }
-  if (st < nsteps) { wave_pair_step<CASE, DIR, 0, false, 2>(x, s, R); ++st; ++R; }
-  if (st < nsteps) { wave_pair_step<CASE, DIR, 1, false, 2>(x, s, R); ++st; ++R; }
-  if (st < nsteps) { wave_pair_step<CASE, DIR, 2, false, 2>(x, s, R); ++st; ++R; }
-  if (st < nsteps) { wave_pair_step<CASE, DIR, 3, false, 2>(x, s, R); ++st; ++R; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 0, false, 2>(x, s, R); ++st; R += DIR; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 1, false, 2>(x, s, R); ++st; R += DIR; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 2, false, 2>(x, s, R); ++st; R += DIR; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 3, false, 2>(x, s, R); ++st; R += DIR; }
   r1 = s.rmax1;
   r2 = s.rmax2;
 }
@@ -1439,10 +1469,27 @@ __device__ __forceinline__ void wave_march_pair_edge(const WaveCtx<CASE>& x, int
 #define CFD_PAIR_MIN_WAVES 2
 #endif
 
+// Tiling of one pair launch. Rows are covered in up to two ranges [lo0, hi0)
+// and [lo1, hi1) (the second may be empty): one launch for a whole strip, or,
+// on ranks that overlap the halo exchange, one launch for the interior rows
+// and one for the rows next to both neighbours. Every column tile splits each
+// range into bands; the first and last column tile (boundary columns, masked
+// march) use shorter bands of `the` rows.
+struct PairPlan {
+  int ctiles;
+  int th, nb0, nb1;    // interior column tiles: band height, bands in range 0 / 1
+  int the, nbe0, nbe1; // boundary column tiles
+  int lo0, hi0, lo1, hi1;
+};
+
 template <int CASE>
 __global__ __launch_bounds__(256, CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
     Geo g, Coef c, const double* __restrict__ pin, double* __restrict__ pout, const double* __restrict__ f,
-    PoissonCtl ctl, int k, int TH, int ctiles, int nbands, int flags) {
+    PoissonCtl ctl, int k, PairPlan pl, int flags) {
+  // tiles: the first and last column tile (boundary columns, general masks)
+  // in bands of pl.the rows, then the interior column tiles in bands of pl.th
+  // rows; the host makes the boundary bands shorter so that their slower
+  // march ends with the others (one resident round)
   constexpr int H = 8;  // column halo (lanes 0-3 and 60-63)
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: band / row logic stays scalar
@@ -1478,12 +1525,27 @@ __global__ __launch_bounds__(256, CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
   const int bl = (int)blockIdx.x;
   const int blk = ((flags & 2) && bl < L8) ? (bl % 8) * (nblk / 8) + bl / 8 : bl;
   const int tile = blk * 4 + wv;
-  if (tile >= ctiles * nbands) return;
-  const int band = tile % nbands, ctile = tile / nbands;
+  const int ne = (pl.ctiles >= 2) ? 2 : 1;
+  const int nbe = pl.nbe0 + pl.nbe1, nbi = pl.nb0 + pl.nb1;
+  int band, ctile, th, nb0;
+  if (tile < ne * nbe) {
+    ctile = (tile < nbe) ? 0 : pl.ctiles - 1;
+    band = tile % nbe;
+    th = pl.the;
+    nb0 = pl.nbe0;
+  } else {
+    const int t = tile - ne * nbe;
+    if (t >= (pl.ctiles - ne) * nbi) return;
+    ctile = 1 + t / nbi;
+    band = t % nbi;
+    th = pl.th;
+    nb0 = pl.nb0;
+  }
   const int gi = ctile * PAIR_TWC - H + 2 * lane;
-  const int y0 = g.wj0 + band * TH;
-  const int y1 = min(y0 + TH, g.wj1 + 1);
-  if (y0 > g.wj1) return;
+  const bool r0 = band < nb0;
+  const int y0 = r0 ? pl.lo0 + band * th : pl.lo1 + (band - nb0) * th;
+  const int y1 = min(y0 + th, r0 ? pl.hi0 : pl.hi1);
+  if (y0 >= y1) return;
   WaveCtx<CASE> x{g, c};
   x.pin = pin; x.pout = pout; x.f = f;
   x.gi = gi;
@@ -1498,20 +1560,20 @@ __global__ __launch_bounds__(256, CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
   x.open_a = (CASE != BACKSTEP) || (gi > c.step_i);
   x.open_b = (CASE != BACKSTEP) || (gi + 1 > c.step_i);
   x.gic = min(max(gi, 0), g.pitch - 2);
-  // interior wave: all 128 columns are fluid cells with fluid neighbours, and
-  // every row of the dependency cone [y0-7, y1+6] is an updated interior row
+  // interior-column wave: all 128 columns are fluid cells with fluid
+  // neighbours (rows are handled row-uniformly inside the fast march)
   const int c0 = ctile * PAIR_TWC - H;
   const bool cols_in = c0 >= 1 && c0 + 127 <= g.nx && (CASE != BACKSTEP || c0 > c.step_i + 1);
-  const bool rows_in = y0 - PAIR_H >= max(1, x.rmin + 1) && y1 + PAIR_H - 1 <= min(g.ny, x.rmax - 1);
   double r1 = 0.0, r2 = 0.0;
   const bool up = (flags & 1) && (band & 1);
   // flags bit 4 / bit 5 (timing diagnostics only): never / always take the interior path
-  const bool fast = (flags & 32) || (!(flags & 16) && cols_in && rows_in);
+  const bool fast = (flags & 32) || (!(flags & 16) && cols_in);
   if (fast) {
     if (up) wave_march_pair<CASE, -1, true>(x, y0, y1, r1, r2);
     else wave_march_pair<CASE, 1, true>(x, y0, y1, r1, r2);
   } else {
-    wave_march_pair_edge<CASE>(x, y0, y1, r1, r2);
+    if (up) wave_march_pair_edge<CASE, -1>(x, y0, y1, r1, r2);
+    else wave_march_pair_edge<CASE, 1>(x, y0, y1, r1, r2);
   }
   r1 = wave_max(r1);
   r2 = wave_max(r2);

@@ -38,6 +38,7 @@ enum { B_P0 = 0, B_P1, B_F, B_US, B_VS, B_U, B_V, B_UC, B_VC, B_PL, NB };  // B_
 
 constexpr int PBX = 64, PBY = 32;  // Poisson tile (fused-tile variant)
 constexpr int MARCH_MIN_TH = 24;   // minimum rows per band (column-march variant)
+constexpr int OVL_ROWS = 16;       // rows next to each neighbour updated by the overlapped boundary launch
 
 struct Strip {
   Geo g{};
@@ -95,10 +96,19 @@ class Solver {
   int* h_stat = nullptr;    // pinned: 2 x {stop, iter}
   double* h_shard = nullptr;  // pinned: RES_SHARDS*SHARD_STRIDE
   hipEvent_t ev_poll[2] = {}, ev_a = nullptr, ev_b = nullptr;
+  // Halo overlap on ranks (RCCL): the rows next to the neighbours and the
+  // exchange run on st_b while the interior rows run on st.
+  hipStream_t st_b = nullptr;
+  hipEvent_t ev_int[2] = {}, ev_bnd[2] = {}, ev_sync = nullptr;
+  bool overlap = false;     // enabled for ranks with enough rows (CFD_OVERLAP=0 disables)
+  bool b_pending = false;   // st_b has work that st has not waited for yet
+  int last_bnd = 0;         // ev_bnd slot recorded last
+  long long n_overlapped = 0;  // overlapped pair launches enqueued (this solve)
   cfd_timing T{};
   int kernel_variant = 0;  // 0: wave march (default), 1: fused LDS tile, 2: block column march
   int resident_waves = 2048;  // wave-march tiles in flight (CUs x 4 SIMDs x waves per SIMD)
   int resident_pair_waves = 2048;  // the same for the two-iteration kernel
+  int pair_edge_pct = 60;          // boundary-column band length, % of the interior march (swept: 55-70 best)
   int resident_blocks = 1024;  // march-kernel blocks resident at once on this device
   int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order
   int march_min_th = MARCH_MIN_TH;
@@ -132,6 +142,7 @@ class Solver {
       HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pps, poisson_pair_kernel<CAVITY>, 256, 0));
       pps = std::max(1, std::min(pps, 4));
       if (const char* e = std::getenv("CFD_PAIR_WPS")) pps = std::max(1, std::atoi(e));
+      if (const char* e = std::getenv("CFD_PAIR_EDGE_PCT")) pair_edge_pct = std::max(10, std::min(100, std::atoi(e)));
       resident_pair_waves = pps * 4 * prop.multiProcessorCount;
       if (const char* e = std::getenv("CFD_MARCH_MIN_TH")) march_min_th = std::max(8, std::atoi(e));
     }
@@ -176,6 +187,19 @@ class Solver {
     for (auto& e : ev_poll) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPC(hipEventCreate(&ev_a));
     HIPC(hipEventCreate(&ev_b));
+    if (comm && comm->nranks > 1 && S.size() == 1) {
+      const Geo& g0 = S[0].g;
+      const char* e = std::getenv("CFD_OVERLAP");
+      overlap = !(e && std::atoi(e) == 0) && (g0.wj1 - g0.wj0 + 1) >= 3 * OVL_ROWS;
+      if (overlap) {
+        HIPC(hipStreamCreateWithFlags(&st_b, hipStreamNonBlocking));
+        for (int q = 0; q < 2; ++q) {
+          HIPC(hipEventCreateWithFlags(&ev_int[q], hipEventDisableTiming));
+          HIPC(hipEventCreateWithFlags(&ev_bnd[q], hipEventDisableTiming));
+        }
+        HIPC(hipEventCreateWithFlags(&ev_sync, hipEventDisableTiming));
+      }
+    }
     // fluid cells (backwards_step-01.cpp:522-528)
     long long solid = 0;
     if (P.case_id == CFD_BACKSTEP)
@@ -199,6 +223,13 @@ class Solver {
       if (e) (void)hipEventDestroy(e);
     if (ev_a) (void)hipEventDestroy(ev_a);
     if (ev_b) (void)hipEventDestroy(ev_b);
+    if (st_b) (void)hipStreamSynchronize(st_b);
+    for (int q = 0; q < 2; ++q) {
+      if (ev_int[q]) (void)hipEventDestroy(ev_int[q]);
+      if (ev_bnd[q]) (void)hipEventDestroy(ev_bnd[q]);
+    }
+    if (ev_sync) (void)hipEventDestroy(ev_sync);
+    if (st_b) (void)hipStreamDestroy(st_b);
     if (st) (void)hipStreamDestroy(st);
   }
 
@@ -226,7 +257,8 @@ class Solver {
 
   // ------------------------------------------------------------ halos --
   // Copy `depth` owned boundary rows of buffer b into the neighbours' halos.
-  void exchange(int b, int depth) {
+  void exchange(int b, int depth, hipStream_t xs = nullptr) {
+    if (!xs) xs = st;
     if (S.size() > 1) {
       for (size_t k = 0; k + 1 < S.size(); ++k) {
         Strip& lo = S[k];
@@ -234,10 +266,10 @@ class Solver {
         const size_t cnt = (size_t)depth * pitch * sizeof(double);
         const int ja = lo.g.j1 - depth + 1;  // lower strip's top rows -> upper's lower halo
         HIPC(hipMemcpyAsync(up.b[b] + (size_t)(ja - up.g.row_lo) * pitch, lo.b[b] + (size_t)(ja - lo.g.row_lo) * pitch,
-                            cnt, hipMemcpyDeviceToDevice, st));
+                            cnt, hipMemcpyDeviceToDevice, xs));
         const int jb = up.g.j0;  // upper strip's bottom rows -> lower's upper halo
         HIPC(hipMemcpyAsync(lo.b[b] + (size_t)(jb - lo.g.row_lo) * pitch, up.b[b] + (size_t)(jb - up.g.row_lo) * pitch,
-                            cnt, hipMemcpyDeviceToDevice, st));
+                            cnt, hipMemcpyDeviceToDevice, xs));
       }
     }
     if (comm && comm->nranks > 1) {
@@ -248,14 +280,14 @@ class Solver {
       auto row = [&](int j) { return base + (size_t)(j - g.row_lo) * pitch; };
       comm_group_start(comm);
       if (comm->rank > 0) {
-        comm_send(comm, row(g.j0), cnt, comm->rank - 1, st);
-        comm_recv(comm, row(g.j0 - depth), cnt, comm->rank - 1, st);
+        comm_send(comm, row(g.j0), cnt, comm->rank - 1, xs);
+        comm_recv(comm, row(g.j0 - depth), cnt, comm->rank - 1, xs);
       }
       if (comm->rank < comm->nranks - 1) {
-        comm_send(comm, row(g.j1 - depth + 1), cnt, comm->rank + 1, st);
-        comm_recv(comm, row(g.j1 + 1), cnt, comm->rank + 1, st);
+        comm_send(comm, row(g.j1 - depth + 1), cnt, comm->rank + 1, xs);
+        comm_recv(comm, row(g.j1 + 1), cnt, comm->rank + 1, xs);
       }
-      comm_group_end(comm, st);
+      comm_group_end(comm, xs);
     }
   }
 
@@ -341,6 +373,40 @@ class Solver {
     nbands = (rows + th - 1) / th;
   }
 
+  // Tiling of a pair launch over rows [lo0, hi0) + [lo1, hi1) with about
+  // `waves` waves (one resident round). Interior column tiles: bands of th
+  // rows; the pair kernel marches in groups of 10 rows over th + 15 rows
+  // (th + 14 + parity alignment), so th = 5 mod 10 wastes no group. The two
+  // boundary column tiles march slower (masks): shorter bands, pair_edge_pct %
+  // of the interior march length.
+  PairPlan pair_plan(int lo0, int hi0, int lo1, int hi1, int waves) const {
+    PairPlan pl{};
+    pl.ctiles = (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC;
+    pl.lo0 = lo0; pl.hi0 = hi0; pl.lo1 = lo1; pl.hi1 = hi1;
+    const int rows = (hi0 - lo0) + (hi1 - lo1);
+    const int ne = pl.ctiles >= 2 ? 2 : 1;
+    const double per = (double)waves / ((pl.ctiles - ne) + ne * 100.0 / pair_edge_pct);
+    const int nb = std::max(1, std::min((int)per, (rows + march_min_th - 1) / march_min_th));
+    const int rmax = std::max(hi0 - lo0, hi1 - lo1);
+    pl.th = std::max(1, std::min(rmax, ((rows + nb - 1) / nb + 4) / 10 * 10 + 5));
+    pl.the = std::max(8, std::min(rmax, (pl.th + 15) * pair_edge_pct / 100 - 14));
+    auto nbands = [](int lo, int hi, int t) { return hi > lo ? (hi - lo + t - 1) / t : 0; };
+    pl.nb0 = nbands(lo0, hi0, pl.th);
+    pl.nb1 = nbands(lo1, hi1, pl.th);
+    pl.nbe0 = nbands(lo0, hi0, pl.the);
+    pl.nbe1 = nbands(lo1, hi1, pl.the);
+    return pl;
+  }
+
+  template <int CASE>
+  void launch_pair(const PairPlan& pl, const Geo& g, const double* pin, double* pout, const double* f,
+                   const PoissonCtl& ctl, int k, hipStream_t stream) {
+    const int ne = pl.ctiles >= 2 ? 2 : 1;
+    const int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
+    if (ntiles == 0) return;
+    poisson_pair_kernel<CASE><<<(ntiles + 3) / 4, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, pl, march_flags);
+  }
+
   // One SOR launch: iteration k (sweeps == 1) or iterations k, k+1 (sweeps == 2).
   // replay: iteration k is already known to be the solve's last (no test).
   template <int CASE>
@@ -351,14 +417,8 @@ class Solver {
       const int rows = g.wj1 - g.wj0 + 1;
       int ctiles, th, nbands;
       if (sweeps == 2) {
-        wave_bands(rows, PAIR_TWC, resident_pair_waves, ctiles, th, nbands);
-        // the pair kernel marches in groups of 10 rows over th + 15 rows
-        // (th + 14 + parity alignment): th = 5 mod 10 wastes no group
-        th = std::min(rows, (th + 4) / 10 * 10 + 5);
-        nbands = (rows + th - 1) / th;
-        const int nblk = (ctiles * nbands + 3) / 4;
-        poisson_pair_kernel<CASE><<<nblk, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k, th, ctiles,
-                                                         nbands, march_flags);
+        const PairPlan pl = pair_plan(g.wj0, g.wj1 + 1, 0, 0, resident_pair_waves / (int)S.size());
+        launch_pair<CASE>(pl, g, pin[q], pout[q], S[q].b[B_F], ctl, k, st);
       } else if (kernel_variant == 1 && !replay) {
         const dim3 grid((P.nx + 2 + PBX - 1) / PBX, (rows + PBY - 1) / PBY);
         poisson_rbsor_kernel<CASE, PBX, PBY><<<grid, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k);
@@ -381,9 +441,73 @@ class Solver {
 
   // SOR launch number m (0-based) of a solve starting in buffer `base`: reads
   // buffer (base+m)&1, writes the other. Iterations k .. k+sweeps-1.
+  // st waits for everything enqueued on st_b so far
+  void join_b() {
+    if (b_pending) {
+      HIPC(hipStreamWaitEvent(st, ev_bnd[last_bnd], 0));
+      b_pending = false;
+    }
+  }
+
+  // Pair launch m on a rank with halo overlap. st_b: exchange of launch m's
+  // input rows, then the rows within OVL_ROWS of each neighbour (their cone
+  // reaches the interior rows of launch m-1: wait for it); st: the interior
+  // rows (they never read halo rows; wait for launch m-1's boundary rows).
+  // The residual all-reduce of the pair follows both, on st_b.
+  template <int CASE>
+  void pair_overlapped(int m, int k, double* pin, double* pout) {
+    const Strip& s = S[0];
+    const Geo& g = s.g;
+    const int lo_b = comm->rank > 0 ? OVL_ROWS : 0;
+    const int hi_b = comm->rank < comm->nranks - 1 ? OVL_ROWS : 0;
+    const int e = m & 1, pe = e ^ 1;
+    PoissonCtl ctl{ring, tolv, stop, P.check_every};
+    if (m == 0) {  // st_b starts after st's work so far (source, tolerance, f halos)
+      HIPC(hipEventRecord(ev_sync, st));
+      HIPC(hipStreamWaitEvent(st_b, ev_sync, 0));
+    }
+    exchange(pin == s.b[B_P0] ? B_P0 : B_P1, HALO, st_b);
+    if (m > 0) HIPC(hipStreamWaitEvent(st_b, ev_int[pe], 0));
+    PairPlan pb{};
+    pb.ctiles = (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC;
+    pb.th = pb.the = OVL_ROWS;
+    pb.lo0 = g.wj0; pb.hi0 = g.wj0 + lo_b;
+    pb.lo1 = g.wj1 + 1 - hi_b; pb.hi1 = g.wj1 + 1;
+    pb.nb0 = pb.nbe0 = lo_b ? 1 : 0;
+    pb.nb1 = pb.nbe1 = hi_b ? 1 : 0;
+    launch_pair<CASE>(pb, g, pin, pout, s.b[B_F], ctl, k, st_b);
+    if (m > 0) HIPC(hipStreamWaitEvent(st, ev_bnd[pe], 0));
+    const PairPlan pi = pair_plan(g.wj0 + lo_b, g.wj1 + 1 - hi_b, 0, 0, resident_pair_waves - 2 * pb.ctiles);
+    launch_pair<CASE>(pi, g, pin, pout, s.b[B_F], ctl, k, st);
+    check_launch("poisson pair (overlapped)");
+    HIPC(hipEventRecord(ev_int[e], st));
+    bool waited = false;
+    for (int kk = k; kk < k + 2; ++kk) {
+      if (kk % P.check_every == 0 || kk == P.max_iters) {
+        if (!waited) HIPC(hipStreamWaitEvent(st_b, ev_int[e], 0));
+        waited = true;
+        double* slot = ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+        comm_allreduce_max(comm, slot, RES_SHARDS * SHARD_STRIDE, st_b);
+      }
+    }
+    HIPC(hipEventRecord(ev_bnd[e], st_b));
+    last_bnd = e;
+    b_pending = true;
+    ++n_overlapped;
+  }
+
   void poisson_launch(int m, int k, int sweeps, int base, bool replay = false, bool after_pair = false) {
     const int bin = ((base + m) & 1) ? B_P1 : B_P0;
     const int bout = ((base + m + 1) & 1) ? B_P1 : B_P0;
+    if (overlap && sweeps == 2 && !replay && kernel_variant == 0) {
+      double* pin = S[0].b[bin];
+      double* pout = S[0].b[bout];
+      if (P.case_id == CFD_CAVITY) pair_overlapped<CAVITY>(m, k, pin, pout);
+      else if (P.case_id == CFD_CHANNEL) pair_overlapped<CHANNEL>(m, k, pin, pout);
+      else pair_overlapped<BACKSTEP>(m, k, pin, pout);
+      return;
+    }
+    join_b();
     if (multi()) exchange(bin, sweeps == 2 ? HALO : 4);
     std::vector<const double*> pin(S.size());
     std::vector<double*> pout(S.size());
@@ -476,6 +600,7 @@ class Solver {
         poisson_launch(m, k + 1, n, base, false, spl == 2 && k > 0);
         k += n;
       }
+      join_b();
       HIPC(hipMemcpyAsync(h_stat + 2 * (c & 1), stop, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
       HIPC(hipEventRecord(ev_poll[c & 1], st));
       if (c > 0) {
@@ -528,6 +653,8 @@ class Solver {
     T.poisson_ms += ms;
     T.poisson_launches += work_launches;
     T.poisson_sweeps += work_sweeps;
+    T.poisson_overlapped += n_overlapped;
+    n_overlapped = 0;
     long long owned = 0;
     for (auto& s : S) owned += (long long)(s.g.j1 - s.g.j0 + 1) * P.nx;
     T.poisson_cell_updates += owned * iters;

@@ -91,6 +91,7 @@ typedef struct cfd_timing {
   double step_ms;             /* device time of whole timesteps */
   long long steps;
   long long poisson_sweeps;   /* SOR iterations executed by those launches (2 per fused launch) */
+  long long poisson_overlapped; /* pair launches split into interior + halo-overlapped boundary rows (ranks) */
 } cfd_timing;
 
 /* Library / ABI info. */

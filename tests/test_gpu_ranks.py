@@ -18,7 +18,7 @@ from cfd_amd import _lib  # noqa: E402
 from cfd_amd.dist import strip_rows  # noqa: E402
 
 
-def run_ranks(cp, world, steps, check_every=1):
+def run_ranks(cp, world, steps, check_every=1, timing=False):
     L = _lib.lib()
     hub = L.cfd_comm_loopback_hub(world)
     assert hub
@@ -35,7 +35,7 @@ def run_ranks(cp, world, steps, check_every=1):
             its = [s.step() for _ in range(steps)]
             md, ke = s.statistics()
             results[r] = dict(rows=s.owned_rows(), u=s.field("u"), v=s.field("v"), p=s.field("p"), its=its,
-                              stats=(md, ke))
+                              stats=(md, ke), overlapped=s.timing().poisson_overlapped)
             s.close()
             L.cfd_comm_destroy(comm)
         except Exception as e:  # noqa: BLE001
@@ -100,3 +100,29 @@ def test_rank_path_check_every_8():
         for (ig, rg), (i1, _r1) in zip(r["its"], its):
             assert i1 <= ig <= i1 + 7
             assert ig % 8 == 0 or ig == cp.max_iters
+
+
+@pytest.mark.parametrize("case,world,ny,steps", [("cavity", 2, 128, 6), ("cavity", 3, 160, 4), ("channel", 2, 128, 4)])
+def test_overlapped_halo_exchange_equals_single_domain(case, world, ny, steps):
+    """Strips of >= 48 rows split each pair launch: the rows within 16 of a
+    neighbour (after the halo exchange) on a second stream, the interior rows
+    concurrently on the first. Must equal one domain (cavity bit for bit)."""
+    cp = C.make_params(case, ny=ny, nx=96)
+    res = run_ranks(cp, world, steps)
+    s, its = single(cp, steps)
+    ref = {n: s.field(n) for n in ("u", "v", "p")}
+    for r in res:
+        assert r["overlapped"] > 0, "overlap path not taken"
+        if case == "cavity":
+            assert r["its"] == its
+        else:
+            assert [i for i, _ in r["its"]] == [i for i, _ in its]
+        j0, j1 = r["rows"]
+        first = 0 if j0 == 1 else j0
+        for n in ("u", "v", "p"):
+            last = min(j1 + 1 if j1 == cp.ny else j1, ref[n].shape[0] - 1)
+            a, b = r[n], ref[n][first:last + 1]
+            if case == "cavity":
+                assert np.array_equal(a.view(np.int64), b.view(np.int64)), (n, r["rows"])
+            else:
+                np.testing.assert_allclose(a, b, rtol=0, atol=1e-9 * max(np.abs(b).max(), 1.0))
