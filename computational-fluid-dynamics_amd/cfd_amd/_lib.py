@@ -14,7 +14,9 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libcfd_amd.so")
+# CFD_AMD_LIB: an alternative in-tree build of the same library (A/B timing of
+# kernel build variants, scripts/); the product default is libcfd_amd.so
+LIB_PATH = os.path.join(PKG_DIR, os.environ.get("CFD_AMD_LIB", "libcfd_amd.so"))
 
 CFD_FIELD = {"p": 0, "src": 1, "us": 3, "vs": 4, "u": 5, "v": 6, "uc": 7, "vc": 8}
 COMM_ID_BYTES = 128

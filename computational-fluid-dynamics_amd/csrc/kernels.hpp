@@ -1337,8 +1337,16 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     if (jout) {
       const double2 m = Q[CFD_SLOT(4 + OFF)], bh = Q[CFD_SLOT(5 + OFF)], ah = Q[CFD_SLOT(3 + OFF)];
       const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
-      if (store && x.out_lane)
-        *reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi) = m;
+      if (store && x.out_lane) {
+        double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
+#ifdef CFD_NT_STORE
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        d2v mv = {m.x, m.y};
+        __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));  // streamed: keep L2 for the re-read halo rows
+#else
+        *dst = m;
+#endif
+      }
       if (FAST) {
         if (j >= x.g.j0 && j <= x.g.j1) {  // row-uniform
           if (CASE == CAVITY && j == ny) {  // top row: eps_n = 0 (cavity-01.cpp:666)
