@@ -778,16 +778,18 @@ __global__ __launch_bounds__(256) void poisson_march_kernel(Geo g, Coef c, const
 // (recomputed), so a wave writes 120 columns. Rows R+1..R+4 of p_in and f
 // are kept in flight in registers.
 
+// bound_ctrl: the lane without a source (0 resp. 63) reads 0, with no
+// zero-initialised destination to merge into (one v_mov_dpp per dword)
 __device__ __forceinline__ double dpp_from_left(double v) {  // lane l receives lane l-1 (wave_shr:1)
   int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_update_dpp(0, lo, 0x138, 0xf, 0xf, false);
-  hi = __builtin_amdgcn_update_dpp(0, hi, 0x138, 0xf, 0xf, false);
+  lo = __builtin_amdgcn_mov_dpp(lo, 0x138, 0xf, 0xf, true);
+  hi = __builtin_amdgcn_mov_dpp(hi, 0x138, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double dpp_from_right(double v) {  // lane l receives lane l+1 (wave_shl:1)
   int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_update_dpp(0, lo, 0x130, 0xf, 0xf, false);
-  hi = __builtin_amdgcn_update_dpp(0, hi, 0x130, 0xf, 0xf, false);
+  lo = __builtin_amdgcn_mov_dpp(lo, 0x130, 0xf, 0xf, true);
+  hi = __builtin_amdgcn_mov_dpp(hi, 0x130, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
 
@@ -959,7 +961,24 @@ struct WaveCtx {
   // interior waves: every column stored, rows clamped (wave-uniform scalar math)
   __device__ double2 ld_fast(const double* base, int R) const {
     const int Rc = min(max(R, rmin), rmax);
-    return *reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * (size_t)g.pitch + gi);
+    const double2* src = reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * (size_t)g.pitch + gi);
+#ifdef CFD_NT_LOAD
+    // rows no other band reads (outside both 14-row band overlaps): streamed
+    if (R >= y0 + 8 && R < y1 - 8) {
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(src));
+      return make_double2(v.x, v.y);
+    }
+#endif
+#ifdef CFD_NT_PIN
+    // p_in streamed (f, re-read by every launch, may then stay in the Infinity Cache)
+    if (base == pin) {
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(src));
+      return make_double2(v.x, v.y);
+    }
+#endif
+    return *src;
   }
 };
 
@@ -1339,7 +1358,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
       const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
       if (store && x.out_lane) {
         double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
-#ifdef CFD_NT_STORE
+#ifndef CFD_NO_NT_STORE
         typedef double d2v __attribute__((ext_vector_type(2)));
         d2v mv = {m.x, m.y};
         __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));  // streamed: keep L2 for the re-read halo rows
@@ -1353,8 +1372,10 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
             rm = fmax(rm, residual_abs<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x));
             rm = fmax(rm, residual_abs<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_res.y));
           } else {
-            rm = fmax(rm, residual_interior<CASE>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x));
-            rm = fmax(rm, residual_interior<CASE>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_res.y));
+            // both cells first: results of arithmetic need no canonicalisation,
+            // so one max per row touches the loop-carried accumulator
+            rm = fmax(rm, fmax(residual_interior<CASE>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x),
+                               residual_interior<CASE>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_res.y)));
           }
         }
       } else if (j >= x.g.j0 && j <= x.g.j1) {
@@ -1543,9 +1564,16 @@ __global__ __launch_bounds__(256, CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
     nb0 = pl.nbe0;
   } else {
     const int t = tile - ne * nbe;
-    if (t >= (pl.ctiles - ne) * nbi) return;
-    ctile = 1 + t / nbi;
-    band = t % nbi;
+    const int nci = pl.ctiles - ne;
+    if (t >= nci * nbi) return;
+    if (flags & 64) {  // band-minor order (diagnostic)
+      ctile = 1 + t / nbi;
+      band = t % nbi;
+    } else {  // column tiles of one band side by side: their shared halo columns
+              // are read at the same moment on the same XCD (one L2)
+      ctile = 1 + t % nci;
+      band = t / nci;
+    }
     th = pl.th;
     nb0 = pl.nb0;
   }
