@@ -108,7 +108,7 @@ class Solver {
   int kernel_variant = 0;  // 0: wave march (default), 1: fused LDS tile, 2: block column march
   int resident_waves = 2048;  // wave-march tiles in flight (CUs x 4 SIMDs x waves per SIMD)
   int resident_pair_waves = 2048;  // the same for the two-iteration kernel
-  int pair_edge_pct = 60;          // boundary-column band length, % of the interior march (swept: 55-70 best)
+  int pair_edge_pct = 53;          // boundary-column band length, % of the interior march (swept: 50-56 best)
   int resident_blocks = 1024;  // march-kernel blocks resident at once on this device
   int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order
   int march_min_th = MARCH_MIN_TH;
@@ -385,16 +385,20 @@ class Solver {
     pl.lo0 = lo0; pl.hi0 = hi0; pl.lo1 = lo1; pl.hi1 = hi1;
     const int rows = (hi0 - lo0) + (hi1 - lo1);
     const int ne = pl.ctiles >= 2 ? 2 : 1;
-    const double per = (double)waves / ((pl.ctiles - ne) + ne * 100.0 / pair_edge_pct);
-    const int nb = std::max(1, std::min((int)per, (rows + march_min_th - 1) / march_min_th));
     const int rmax = std::max(hi0 - lo0, hi1 - lo1);
-    pl.th = std::max(1, std::min(rmax, ((rows + nb - 1) / nb + 4) / 10 * 10 + 5));
-    pl.the = std::max(8, std::min(rmax, (pl.th + 15) * pair_edge_pct / 100 - 14));
     auto nbands = [](int lo, int hi, int t) { return hi > lo ? (hi - lo + t - 1) / t : 0; };
-    pl.nb0 = nbands(lo0, hi0, pl.th);
-    pl.nb1 = nbands(lo1, hi1, pl.th);
-    pl.nbe0 = nbands(lo0, hi0, pl.the);
-    pl.nbe1 = nbands(lo1, hi1, pl.the);
+    // most interior bands whose tiles (boundary tiles included) all fit in one round
+    int nb = std::max(1, std::min(waves / std::max(1, pl.ctiles), (rows + march_min_th - 1) / march_min_th));
+    for (;; --nb) {
+      pl.th = std::max(1, std::min(rmax, ((rows + nb - 1) / nb + 4) / 10 * 10 + 5));
+      pl.the = std::max(8, std::min(rmax, (pl.th + 15) * pair_edge_pct / 100 - 14));
+      pl.nb0 = nbands(lo0, hi0, pl.th);
+      pl.nb1 = nbands(lo1, hi1, pl.th);
+      pl.nbe0 = nbands(lo0, hi0, pl.the);
+      pl.nbe1 = nbands(lo1, hi1, pl.the);
+      const int tiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
+      if (tiles <= waves || nb == 1) break;
+    }
     return pl;
   }
 
