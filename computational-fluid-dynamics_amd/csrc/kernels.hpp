@@ -1219,6 +1219,9 @@ constexpr int PAIR_TWC = 128 - 2 * 8;         // output columns per wave (8-colu
 
 #define CFD_SLOT(X) ((((ROT) + 4 - (X)) % 5 + 10) % 5)
 
+// NPR: slots of the prefetch rings (rows in flight = NPR - 1); 5 or 10 (the
+// unrolled march covers 10 rows, so both return to the same slots)
+template <int NPR>
 struct WavePair {
   double2 w[5];   // iteration k, post-black rows R-4d .. R
   double2 q[5];   // iteration k, final rows R-5d .. R-3d
@@ -1226,10 +1229,14 @@ struct WavePair {
   double2 q2[5];  // iteration k+1, final rows R-8d .. R-6d
   double2 fr[5];  // source rows R-d .. R-5d
   double2 fr2[5]; // source rows R-6d .. R-10d
-  double2 np[5];  // prefetched p_in rows R .. R+4d
-  double2 nf[5];  // prefetched f rows R-d .. R+3d
+  double2 np[NPR];  // prefetched p_in rows R .. R+(NPR-1)d
+  double2 nf[NPR];  // prefetched f rows R-d .. R+(NPR-2)d
   double rmax1, rmax2;
 };
+
+#ifndef CFD_PAIR_NPR
+#define CFD_PAIR_NPR 5
+#endif
 
 // Interior SOR update / residual magnitude: every neighbour is a fluid cell
 // (cavity: all four indicators are 1, so the reference's products are the
@@ -1392,18 +1399,24 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
 #undef CFD_N
 }
 
-template <int CASE, int DIR, int ROT, bool FAST, int PAR>  // PAR = parity of R (2: not known at compile time)
-__device__ __forceinline__ void wave_pair_step(const WaveCtx<CASE>& x, WavePair& s, int R) {
-  // consume the prefetched row R (and f row R-d); issue the loads 4 rows ahead
+// slot of row R - X*d in a prefetch ring of NPR slots at march step t (t mod
+// 10 from ROT = t mod 5 and PAR = t mod 2; NPR == 5 only needs ROT)
+#define CFD_NSLOT(X) ((NPR == 5) ? CFD_SLOT(X) : ((((6 * (ROT) + 5 * (PAR)) % 10 + NPR - 1 - (X)) % NPR + 2 * NPR) % NPR))
+
+template <int CASE, int DIR, int ROT, bool FAST, int PAR, int NPR>  // PAR = parity of R (2: not known at compile time)
+__device__ __forceinline__ void wave_pair_step(const WaveCtx<CASE>& x, WavePair<NPR>& s, int R) {
+  constexpr int PD = NPR - 1;  // rows in flight ahead of the front row
+  static_assert(NPR == 5 || PAR != 2, "deep prefetch rings need the 10-step unroll");
+  // consume the prefetched row R (and f row R-d); issue the loads PD rows ahead
   s.fr2[CFD_SLOT(6)] = s.fr[CFD_SLOT(6)];  // f row R-6d leaves fr (its slot takes row R-d) for fr2
-  s.w[CFD_SLOT(0)] = s.np[CFD_SLOT(0)];
-  s.fr[CFD_SLOT(1)] = s.nf[CFD_SLOT(0)];
+  s.w[CFD_SLOT(0)] = s.np[CFD_NSLOT(0)];
+  s.fr[CFD_SLOT(1)] = s.nf[CFD_NSLOT(0)];
   if (FAST) {  // rows clamped to stored memory (wave-uniform); out-of-range rows are never consumed
-    s.np[CFD_SLOT(-4)] = x.ld_fast(x.pin, R + 4 * DIR);
-    s.nf[CFD_SLOT(-4)] = x.ld_fast(x.f, R + 3 * DIR);
+    s.np[CFD_NSLOT(-PD)] = x.ld_fast(x.pin, R + PD * DIR);
+    s.nf[CFD_NSLOT(-PD)] = x.ld_fast(x.f, R + (PD - 1) * DIR);
   } else {
-    s.np[CFD_SLOT(-4)] = x.ld(x.pin, R + 4 * DIR);
-    s.nf[CFD_SLOT(-4)] = x.ld(x.f, R + 3 * DIR);
+    s.np[CFD_NSLOT(-PD)] = x.ld(x.pin, R + PD * DIR);
+    s.nf[CFD_NSLOT(-PD)] = x.ld(x.f, R + (PD - 1) * DIR);
   }
   // iteration k: rows R-d .. R-4d
   pair_stages<CASE, DIR, ROT, 0, FAST, PAR>(x, s.w, s.q, s.fr[CFD_SLOT(1)], s.fr[CFD_SLOT(2)], s.fr[CFD_SLOT(4)], R, false,
@@ -1425,31 +1438,32 @@ __device__ __forceinline__ void wave_march_pair(const WaveCtx<CASE>& x, int y0, 
   const int Rb0 = (DIR > 0) ? y0 - H : y1 - 1 + H;
   const int Rbeg = Rb0 - DIR * (Rb0 & 1);
   const int nsteps = (y1 - y0) + 2 * H + (Rb0 & 1);
-  WavePair s;
+  constexpr int NPR = FAST ? CFD_PAIR_NPR : 5;
+  WavePair<NPR> s;
   const double2 z = make_double2(0.0, 0.0);
 #pragma unroll
   for (int k = 0; k < 5; ++k) s.w[k] = s.q[k] = s.w2[k] = s.q2[k] = s.fr[k] = s.fr2[k] = z;
   s.rmax1 = s.rmax2 = 0.0;
   {
-    constexpr int ROT = 0;  // slots as seen by the first step
+    constexpr int ROT = 0, PAR = 0;  // slots as seen by the first step
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      s.np[CFD_SLOT(-q)] = FAST ? x.ld_fast(x.pin, Rbeg + q * DIR) : x.ld(x.pin, Rbeg + q * DIR);
-      s.nf[CFD_SLOT(-q)] = FAST ? x.ld_fast(x.f, Rbeg + (q - 1) * DIR) : x.ld(x.f, Rbeg + (q - 1) * DIR);
+    for (int q = 0; q < NPR - 1; ++q) {
+      s.np[CFD_NSLOT(-q)] = FAST ? x.ld_fast(x.pin, Rbeg + q * DIR) : x.ld(x.pin, Rbeg + q * DIR);
+      s.nf[CFD_NSLOT(-q)] = FAST ? x.ld_fast(x.f, Rbeg + (q - 1) * DIR) : x.ld(x.f, Rbeg + (q - 1) * DIR);
     }
   }
   int R = Rbeg;
   for (int st = 0; st < nsteps; st += 10, R += 10 * DIR) {
-    wave_pair_step<CASE, DIR, 0, FAST, 0>(x, s, R);
-    wave_pair_step<CASE, DIR, 1, FAST, 1>(x, s, R + DIR);
-    wave_pair_step<CASE, DIR, 2, FAST, 0>(x, s, R + 2 * DIR);
-    wave_pair_step<CASE, DIR, 3, FAST, 1>(x, s, R + 3 * DIR);
-    wave_pair_step<CASE, DIR, 4, FAST, 0>(x, s, R + 4 * DIR);
-    wave_pair_step<CASE, DIR, 0, FAST, 1>(x, s, R + 5 * DIR);
-    wave_pair_step<CASE, DIR, 1, FAST, 0>(x, s, R + 6 * DIR);
-    wave_pair_step<CASE, DIR, 2, FAST, 1>(x, s, R + 7 * DIR);
-    wave_pair_step<CASE, DIR, 3, FAST, 0>(x, s, R + 8 * DIR);
-    wave_pair_step<CASE, DIR, 4, FAST, 1>(x, s, R + 9 * DIR);
+    wave_pair_step<CASE, DIR, 0, FAST, 0, NPR>(x, s, R);
+    wave_pair_step<CASE, DIR, 1, FAST, 1, NPR>(x, s, R + DIR);
+    wave_pair_step<CASE, DIR, 2, FAST, 0, NPR>(x, s, R + 2 * DIR);
+    wave_pair_step<CASE, DIR, 3, FAST, 1, NPR>(x, s, R + 3 * DIR);
+    wave_pair_step<CASE, DIR, 4, FAST, 0, NPR>(x, s, R + 4 * DIR);
+    wave_pair_step<CASE, DIR, 0, FAST, 1, NPR>(x, s, R + 5 * DIR);
+    wave_pair_step<CASE, DIR, 1, FAST, 0, NPR>(x, s, R + 6 * DIR);
+    wave_pair_step<CASE, DIR, 2, FAST, 1, NPR>(x, s, R + 7 * DIR);
+    wave_pair_step<CASE, DIR, 3, FAST, 0, NPR>(x, s, R + 8 * DIR);
+    wave_pair_step<CASE, DIR, 4, FAST, 1, NPR>(x, s, R + 9 * DIR);
   }
   r1 = FAST ? (x.out_lane ? s.rmax1 : 0.0) : s.rmax1;
   r2 = FAST ? (x.out_lane ? s.rmax2 : 0.0) : s.rmax2;
@@ -1464,7 +1478,8 @@ __device__ __forceinline__ void wave_march_pair_edge(const WaveCtx<CASE>& x, int
   constexpr int H = PAIR_H;
   const int Rbeg = (DIR > 0) ? y0 - H : y1 - 1 + H;
   const int nsteps = (y1 - y0) + 2 * H;
-  WavePair s;
+  constexpr int NPR = 5;
+  WavePair<NPR> s;
   const double2 z = make_double2(0.0, 0.0);
 #pragma unroll
   for (int k = 0; k < 5; ++k) s.w[k] = s.q[k] = s.w2[k] = s.q2[k] = s.fr[k] = s.fr2[k] = z;
@@ -1479,19 +1494,20 @@ __device__ __forceinline__ void wave_march_pair_edge(const WaveCtx<CASE>& x, int
   }
   int st = 0, R = Rbeg;
   for (; st + 5 <= nsteps; st += 5, R += 5 * DIR) {
-    wave_pair_step<CASE, DIR, 0, false, 2>(x, s, R);
-    wave_pair_step<CASE, DIR, 1, false, 2>(x, s, R + DIR);
-    wave_pair_step<CASE, DIR, 2, false, 2>(x, s, R + 2 * DIR);
-    wave_pair_step<CASE, DIR, 3, false, 2>(x, s, R + 3 * DIR);
-    wave_pair_step<CASE, DIR, 4, false, 2>(x, s, R + 4 * DIR);
+    wave_pair_step<CASE, DIR, 0, false, 2, 5>(x, s, R);
+    wave_pair_step<CASE, DIR, 1, false, 2, 5>(x, s, R + DIR);
+    wave_pair_step<CASE, DIR, 2, false, 2, 5>(x, s, R + 2 * DIR);
+    wave_pair_step<CASE, DIR, 3, false, 2, 5>(x, s, R + 3 * DIR);
+    wave_pair_step<CASE, DIR, 4, false, 2, 5>(x, s, R + 4 * DIR);
   }
-  if (st < nsteps) { wave_pair_step<CASE, DIR, 0, false, 2>(x, s, R); ++st; R += DIR; }
-  if (st < nsteps) { wave_pair_step<CASE, DIR, 1, false, 2>(x, s, R); ++st; R += DIR; }
-  if (st < nsteps) { wave_pair_step<CASE, DIR, 2, false, 2>(x, s, R); ++st; R += DIR; }
-  if (st < nsteps) { wave_pair_step<CASE, DIR, 3, false, 2>(x, s, R); ++st; R += DIR; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 0, false, 2, 5>(x, s, R); ++st; R += DIR; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 1, false, 2, 5>(x, s, R); ++st; R += DIR; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 2, false, 2, 5>(x, s, R); ++st; R += DIR; }
+  if (st < nsteps) { wave_pair_step<CASE, DIR, 3, false, 2, 5>(x, s, R); ++st; R += DIR; }
   r1 = s.rmax1;
   r2 = s.rmax2;
 }
+#undef CFD_NSLOT
 #undef CFD_SLOT
 
 #ifndef CFD_PAIR_MIN_WAVES
