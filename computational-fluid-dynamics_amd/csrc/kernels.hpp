@@ -1530,7 +1530,7 @@ struct PairPlan {
 template <int CASE>
 __global__ __launch_bounds__(256, CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
     Geo g, Coef c, const double* __restrict__ pin, double* __restrict__ pout, const double* __restrict__ f,
-    PoissonCtl ctl, int k, PairPlan pl, int flags) {
+    PoissonCtl ctl, int k, int lag, PairPlan pl, int flags) {
   // tiles: the first and last column tile (boundary columns, general masks)
   // in bands of pl.the rows, then the interior column tiles in bands of pl.th
   // rows; the host makes the boundary bands shorter so that their slower
@@ -1539,19 +1539,18 @@ __global__ __launch_bounds__(256, CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: band / row logic stays scalar
 
-  // convergence tests of iterations k-2 and k-1 (all waves agree): the first
-  // that meets the tolerance (on a checked iteration) ends the solve there
+  // convergence tests of the previous pair's iterations k-2, k-1 (lag 1: of
+  // the pair before, k-4, k-3; iteration 0 = the initial residual), all waves
+  // agree: the first that meets the tolerance (on a tested iteration) ends the
+  // solve there
   {
     const double tol = ctl.tol[0];
     if (ctl.stop[0] != 0) return;
     int stop_at = -1;
-    if (k == 1) {
-      if (!pair_go_on(ctl, 0, lane, tol)) stop_at = 0;
-    } else {
-      const int ka = k - 2, kb = k - 1;
-      if (ka >= 1 && ka % ctl.check_every == 0 && !pair_go_on(ctl, ka, lane, tol)) stop_at = ka;
-      else if (kb % ctl.check_every == 0 && !pair_go_on(ctl, kb, lane, tol)) stop_at = kb;
-    }
+    const int ka = k - 2 - 2 * lag, kb = k - 1 - 2 * lag;
+    auto tested = [&](int kk) { return kk == 0 || (kk >= 1 && kk % ctl.check_every == 0); };
+    if (tested(ka) && !pair_go_on(ctl, ka, lane, tol)) stop_at = ka;
+    else if (tested(kb) && !pair_go_on(ctl, kb, lane, tol)) stop_at = kb;
     if (stop_at >= 0) {
       if (lane == 0 && wv == 0 && blockIdx.x == 0) {
         ctl.stop[1] = stop_at;

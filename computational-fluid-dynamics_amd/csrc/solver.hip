@@ -34,7 +34,9 @@ static void check_launch(const char* what) {
   if (e != hipSuccess) throw Error(CFD_E_DEVICE, std::string("launch ") + what + ": " + hipGetErrorString(e));
 }
 
-enum { B_P0 = 0, B_P1, B_F, B_US, B_VS, B_U, B_V, B_UC, B_VC, B_PL, NB };  // B_PL: lex-mode initial field
+enum { B_P0 = 0, B_P1, B_F, B_US, B_VS, B_U, B_V, B_UC, B_VC, B_PL, B_P2, NB };  // B_PL: lex-mode initial field;
+// B_P2: third pressure buffer of the lagged convergence test (ranks)
+static int pbuf(int idx) { return idx == 0 ? B_P0 : idx == 1 ? B_P1 : B_P2; }
 
 constexpr int PBX = 64, PBY = 32;  // Poisson tile (fused-tile variant)
 constexpr int MARCH_MIN_TH = 24;   // minimum rows per band (column-march variant)
@@ -85,7 +87,7 @@ class Solver {
   hipStream_t st = nullptr;
   std::vector<Strip> S;
   Comm* comm = nullptr;  // non-null: this process is one rank of a strip decomposition
-  int pcur = 0;          // which p buffer holds the current pressure
+  int pcur = 0;          // which p buffer (pbuf index) holds the current pressure
   int pitch = 0;
   double fluid_count = 0;
 
@@ -101,6 +103,12 @@ class Solver {
   hipStream_t st_b = nullptr;
   hipEvent_t ev_int[2] = {}, ev_bnd[2] = {}, ev_sync = nullptr;
   bool overlap = false;     // enabled for ranks with enough rows (CFD_OVERLAP=0 disables)
+  // With overlap the convergence test lags one more pair: launch m tests the
+  // residuals of pair m-2, whose all-reduce then runs beside launch m-1
+  // instead of in front of launch m. A third pressure buffer keeps the input
+  // and output of the pair a late stop lands in intact.
+  bool lagged() const { return overlap && P.sweeps_per_launch != 1 && kernel_variant == 0; }
+  int nbufs() const { return lagged() ? 3 : 2; }
   bool b_pending = false;   // st_b has work that st has not waited for yet
   int last_bnd = 0;         // ev_bnd slot recorded last
   long long n_overlapped = 0;  // overlapped pair launches enqueued (this solve)
@@ -404,11 +412,12 @@ class Solver {
 
   template <int CASE>
   void launch_pair(const PairPlan& pl, const Geo& g, const double* pin, double* pout, const double* f,
-                   const PoissonCtl& ctl, int k, hipStream_t stream) {
+                   const PoissonCtl& ctl, int k, hipStream_t stream, int lag = 0) {
     const int ne = pl.ctiles >= 2 ? 2 : 1;
     const int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
     if (ntiles == 0) return;
-    poisson_pair_kernel<CASE><<<(ntiles + 3) / 4, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, pl, march_flags);
+    poisson_pair_kernel<CASE><<<(ntiles + 3) / 4, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, lag, pl,
+                                                                    march_flags);
   }
 
   // One SOR launch: iteration k (sweeps == 1) or iterations k, k+1 (sweeps == 2).
@@ -458,9 +467,21 @@ class Solver {
   // reaches the interior rows of launch m-1: wait for it); st: the interior
   // rows (they never read halo rows; wait for launch m-1's boundary rows).
   // The residual all-reduce of the pair follows both, on st_b.
+  // all-reduce (max) of the residual slots of iterations k, k+1 that are tested
+  void allreduce_pair_slots(int k, hipStream_t xs) {
+    for (int kk = k; kk < k + 2 && kk <= P.max_iters; ++kk) {
+      if (kk % P.check_every == 0 || kk == P.max_iters) {
+        double* slot = ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+        comm_allreduce_max(comm, slot, RES_SHARDS * SHARD_STRIDE, xs);
+      }
+    }
+  }
+
   template <int CASE>
-  void pair_overlapped(int m, int k, double* pin, double* pout) {
+  void pair_overlapped(int m, int k, int bin, int bout) {
     const Strip& s = S[0];
+    double* pin = s.b[bin];
+    double* pout = s.b[bout];
     const Geo& g = s.g;
     const int lo_b = comm->rank > 0 ? OVL_ROWS : 0;
     const int hi_b = comm->rank < comm->nranks - 1 ? OVL_ROWS : 0;
@@ -470,8 +491,11 @@ class Solver {
       HIPC(hipEventRecord(ev_sync, st));
       HIPC(hipStreamWaitEvent(st_b, ev_sync, 0));
     }
-    exchange(pin == s.b[B_P0] ? B_P0 : B_P1, HALO, st_b);
-    if (m > 0) HIPC(hipStreamWaitEvent(st_b, ev_int[pe], 0));
+    exchange(bin, HALO, st_b);
+    if (m > 0) {
+      HIPC(hipStreamWaitEvent(st_b, ev_int[pe], 0));
+      allreduce_pair_slots(k - 2, st_b);  // pair m-1, tested by launch m+1
+    }
     PairPlan pb{};
     pb.ctiles = (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC;
     pb.th = pb.the = OVL_ROWS;
@@ -479,21 +503,12 @@ class Solver {
     pb.lo1 = g.wj1 + 1 - hi_b; pb.hi1 = g.wj1 + 1;
     pb.nb0 = pb.nbe0 = lo_b ? 1 : 0;
     pb.nb1 = pb.nbe1 = hi_b ? 1 : 0;
-    launch_pair<CASE>(pb, g, pin, pout, s.b[B_F], ctl, k, st_b);
+    launch_pair<CASE>(pb, g, pin, pout, s.b[B_F], ctl, k, st_b, 1);
     if (m > 0) HIPC(hipStreamWaitEvent(st, ev_bnd[pe], 0));
     const PairPlan pi = pair_plan(g.wj0 + lo_b, g.wj1 + 1 - hi_b, 0, 0, resident_pair_waves - 2 * pb.ctiles);
-    launch_pair<CASE>(pi, g, pin, pout, s.b[B_F], ctl, k, st);
+    launch_pair<CASE>(pi, g, pin, pout, s.b[B_F], ctl, k, st, 1);
     check_launch("poisson pair (overlapped)");
     HIPC(hipEventRecord(ev_int[e], st));
-    bool waited = false;
-    for (int kk = k; kk < k + 2; ++kk) {
-      if (kk % P.check_every == 0 || kk == P.max_iters) {
-        if (!waited) HIPC(hipStreamWaitEvent(st_b, ev_int[e], 0));
-        waited = true;
-        double* slot = ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-        comm_allreduce_max(comm, slot, RES_SHARDS * SHARD_STRIDE, st_b);
-      }
-    }
     HIPC(hipEventRecord(ev_bnd[e], st_b));
     last_bnd = e;
     b_pending = true;
@@ -501,17 +516,16 @@ class Solver {
   }
 
   void poisson_launch(int m, int k, int sweeps, int base, bool replay = false, bool after_pair = false) {
-    const int bin = ((base + m) & 1) ? B_P1 : B_P0;
-    const int bout = ((base + m + 1) & 1) ? B_P1 : B_P0;
+    const int bin = pbuf((base + m) % nbufs());
+    const int bout = pbuf((base + m + 1) % nbufs());
     if (overlap && sweeps == 2 && !replay && kernel_variant == 0) {
-      double* pin = S[0].b[bin];
-      double* pout = S[0].b[bout];
-      if (P.case_id == CFD_CAVITY) pair_overlapped<CAVITY>(m, k, pin, pout);
-      else if (P.case_id == CFD_CHANNEL) pair_overlapped<CHANNEL>(m, k, pin, pout);
-      else pair_overlapped<BACKSTEP>(m, k, pin, pout);
+      if (P.case_id == CFD_CAVITY) pair_overlapped<CAVITY>(m, k, bin, bout);
+      else if (P.case_id == CFD_CHANNEL) pair_overlapped<CHANNEL>(m, k, bin, bout);
+      else pair_overlapped<BACKSTEP>(m, k, bin, bout);
       return;
     }
     join_b();
+    const bool notest = lagged() && !replay;  // lagged mode: a single launch tests nothing (the host does)
     if (multi()) exchange(bin, sweeps == 2 ? HALO : 4);
     std::vector<const double*> pin(S.size());
     std::vector<double*> pout(S.size());
@@ -519,9 +533,10 @@ class Solver {
       pin[q] = S[q].b[bin];
       pout[q] = S[q].b[bout];
     }
-    if (P.case_id == CFD_CAVITY) launch_poisson<CAVITY>(pin.data(), pout.data(), k, sweeps, replay, after_pair);
-    else if (P.case_id == CFD_CHANNEL) launch_poisson<CHANNEL>(pin.data(), pout.data(), k, sweeps, replay, after_pair);
-    else launch_poisson<BACKSTEP>(pin.data(), pout.data(), k, sweeps, replay, after_pair);
+    const bool skip = replay || notest;  // launch without the convergence test
+    if (P.case_id == CFD_CAVITY) launch_poisson<CAVITY>(pin.data(), pout.data(), k, sweeps, skip, after_pair);
+    else if (P.case_id == CFD_CHANNEL) launch_poisson<CHANNEL>(pin.data(), pout.data(), k, sweeps, skip, after_pair);
+    else launch_poisson<BACKSTEP>(pin.data(), pout.data(), k, sweeps, skip, after_pair);
     if (comm && comm->nranks > 1 && !replay) {
       for (int kk = k; kk < k + sweeps; ++kk) {
         if (kk % P.check_every == 0 || kk == P.max_iters) {
@@ -540,8 +555,8 @@ class Solver {
     Strip& s = S[0];
     const int base = pcur;
     const size_t bytes = (size_t)s.g.nrows * pitch * sizeof(double);
-    double* X0 = s.b[base ? B_P1 : B_P0];
-    double* X1 = s.b[base ? B_P0 : B_P1];
+    double* X0 = s.b[pbuf(base)];       // (lex: single strip, no ranks -> two buffers)
+    double* X1 = s.b[pbuf(base ^ 1)];
     if (P.case_id == CFD_CAVITY) {  // cavity-01.cpp:610-611: zero field, zero ghosts
       HIPC(hipMemsetAsync(X0, 0, bytes, st));
       HIPC(hipMemsetAsync(X1, 0, bytes, st));
@@ -587,7 +602,7 @@ class Solver {
     if (P.case_id == CFD_CAVITY) {
       // cavity-01.cpp:610-611: each solve starts from a zero field
       for (auto& s : S)
-        HIPC(hipMemsetAsync(s.b[base ? B_P1 : B_P0], 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
+        HIPC(hipMemsetAsync(s.b[pbuf(base)], 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
     }
     solve_tolerance();
     if (multi()) exchange(B_F, HALO - 1);
@@ -597,11 +612,15 @@ class Solver {
     const int chunk = P.chunk > 0 ? P.chunk : 32;  // launches between host polls
     HIPC(hipEventRecord(ev_a, st));
     int k = 0, c = 0, m = 0;
+    int last_tested = -1;  // highest iteration whose residual a launch tests (0: the initial one)
+    const int lag = lagged() ? 1 : 0;
     bool stopped = false;
     while (k < P.max_iters && !stopped) {
       for (int j = 0; j < chunk && k < P.max_iters; ++j, ++m) {
         const int n = std::min(spl, P.max_iters - k);
         poisson_launch(m, k + 1, n, base, false, spl == 2 && k > 0);
+        if (n == 2) last_tested = std::max(last_tested, k - 2 * lag);
+        else if (!lag) last_tested = std::max(last_tested, k);
         k += n;
       }
       join_b();
@@ -612,6 +631,10 @@ class Solver {
         if (h_stat[2 * ((c - 1) & 1)] != 0) stopped = true;
       }
       ++c;
+    }
+    if (lagged() && k >= 2) {  // the last pair's all-reduce (no later launch enqueued it)
+      const int klast = (P.max_iters & 1) && k == P.max_iters ? k - 2 : k - 1;
+      allreduce_pair_slots(klast, st);
     }
     HIPC(hipEventRecord(ev_b, st));
     int iters;
@@ -625,17 +648,29 @@ class Solver {
     HIPC(hipEventSynchronize(ev_b));
     float ms = 0.f;
     HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
-    // iteration max_iters-1 ran as the first of the last pair: no later launch
-    // tested it, so test it here (the reference's while condition)
-    if (spl == 2 && iters == P.max_iters && P.max_iters >= 2 && P.max_iters % 2 == 0 &&
-        (P.max_iters - 1) % P.check_every == 0) {
+    // iterations after the last one a launch tested (the last pair(s), and the
+    // initial residual if no launch tested it): test them here, in order (the
+    // reference's while condition, cavity-01.cpp:633)
+    if (iters == P.max_iters && last_tested < P.max_iters - 1) {
       double t2[2];
       HIPC(hipMemcpy(t2, tolv, sizeof t2, hipMemcpyDeviceToHost));
-      const double* slot = ring + (size_t)((P.max_iters - 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-      HIPC(hipMemcpy(h_shard, slot, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost));
-      double r = 0.0;
-      for (int q = 0; q < RES_SHARDS; ++q) r = std::max(r, h_shard[q * SHARD_STRIDE]);
-      if (!(r > t2[0])) iters = P.max_iters - 1;
+      for (int kk = last_tested + 1; kk <= P.max_iters - 1; ++kk) {
+        double r;
+        if (kk == 0) {
+          r = t2[1];
+        } else if (kk % P.check_every == 0) {
+          const double* slot = ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+          HIPC(hipMemcpy(h_shard, slot, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost));
+          r = 0.0;
+          for (int q = 0; q < RES_SHARDS; ++q) r = std::max(r, h_shard[q * SHARD_STRIDE]);
+        } else {
+          continue;
+        }
+        if (!(r > t2[0])) {
+          iters = kk;
+          break;
+        }
+      }
     }
     // an odd last iteration that ran as the first of a pair: its pair wrote
     // iteration iters+1; recompute iteration iters from the pair's input
@@ -673,10 +708,10 @@ class Solver {
       res = 0.0;
       for (int q = 0; q < RES_SHARDS; ++q) res = std::max(res, h_shard[q * SHARD_STRIDE]);
     }
-    // launch m's output is buffer (base+m+1)&1; iteration `iters` was written by
-    // launch ceil(iters/spl)-1 (or its replay, into the same buffer)
+    // launch m's output is buffer (base+m+1) mod nbufs; iteration `iters` was
+    // written by launch ceil(iters/spl)-1 (or its replay, into the same buffer)
     const int last_launch = (iters + spl - 1) / spl;
-    pcur = (base + last_launch) & 1;
+    pcur = (base + last_launch) % nbufs();
     if (out) {
       out->sor_iterations = iters;
       out->residual = res;
@@ -684,7 +719,7 @@ class Solver {
   }
 
   void correct() {
-    const int bp = pcur ? B_P1 : B_P0;
+    const int bp = pbuf(pcur);
     if (multi()) exchange(bp, 1);
     for (auto& s : S) {
       correct_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_US], s.b[B_VS], s.b[B_U], s.b[B_V]);
@@ -743,7 +778,7 @@ class Solver {
   // ------------------------------------------------------ field access --
   int field_buf(int field) const {
     switch (field) {
-      case CFD_FIELD_P: return pcur ? B_P1 : B_P0;
+      case CFD_FIELD_P: return pbuf(pcur);
       case CFD_FIELD_SRC: return B_F;
       case CFD_FIELD_US: return B_US;
       case CFD_FIELD_VS: return B_VS;

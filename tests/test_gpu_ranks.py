@@ -126,3 +126,26 @@ def test_overlapped_halo_exchange_equals_single_domain(case, world, ny, steps):
                 assert np.array_equal(a.view(np.int64), b.view(np.int64)), (n, r["rows"])
             else:
                 np.testing.assert_allclose(a, b, rtol=0, atol=1e-9 * max(np.abs(b).max(), 1.0))
+
+
+@pytest.mark.parametrize("delta", [-2, -1, 0, 1, 2, 3])
+def test_overlapped_lagged_stop_and_caps(delta):
+    """Overlapped ranks test the residuals one pair late (their all-reduce runs
+    beside the next launch) and keep three pressure buffers: a stop at an odd
+    or even count, a cap just below / at / above the natural stop K, and the
+    host's test of the last untested iterations must all give the
+    single-domain iteration count and field."""
+    base = C.make_params("cavity", ny=128, nx=96)
+    s0, its0 = single(base, 1)
+    K = its0[0][0]
+    cp = C.make_params("cavity", ny=128, nx=96, max_iters=max(1, K + delta))
+    res = run_ranks(cp, 2, 2)
+    s, its = single(cp, 2)
+    ref = s.field("p")
+    for r in res:
+        assert r["overlapped"] > 0
+        assert r["its"] == its, (K, delta)
+        j0, j1 = r["rows"]
+        first = 0 if j0 == 1 else j0
+        last = min(j1 + 1 if j1 == cp.ny else j1, ref.shape[0] - 1)
+        assert np.array_equal(r["p"].view(np.int64), ref[first:last + 1].view(np.int64))
