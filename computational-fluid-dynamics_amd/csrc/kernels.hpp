@@ -1469,6 +1469,137 @@ __device__ __forceinline__ void wave_march_pair(const WaveCtx<CASE>& x, int y0, 
   r2 = FAST ? (x.out_lane ? s.rmax2 : 0.0) : s.rmax2;
 }
 
+// ---- cavity interior waves: a shorter pipeline (dependency depth 5) -------
+//
+// The cavity has no ghost / solid refresh (its ghosts are fixed zeros), so a
+// row is final as soon as its black cells are updated: iteration k updates
+// red at R-1, black at R-2 and takes the residual at R-3; iteration k+1
+// takes row R-2 as its front row (red R-3, black R-4, residual + store R-5).
+// Same operations in the same order per cell as the general pipeline (bit-
+// identical); 5 halo rows instead of 7, and no final-value or second source
+// ring (fewer VGPRs).
+constexpr int CAV_H = 5;
+
+template <int NPR>
+struct CavPair {
+  double2 w[5];    // iteration k (final after black), rows R-4d .. R
+  double2 w2[5];   // iteration k+1, rows R-6d .. R-2d
+  double2 fr[5];   // source rows R-d .. R-5d
+  double2 np[NPR]; // prefetched p_in rows R .. R+(NPR-1)d
+  double2 nf[NPR]; // prefetched f rows R-d .. R+(NPR-2)d
+  double rmax1, rmax2;
+};
+
+// red (COLOR 0) / black (COLOR 1) update of row j = R - X*d on a ring; j's
+// parity is JPAR (compile time)
+template <int DIR, int ROT, int JPAR, int COLOR>
+__device__ __forceinline__ void cav_update(const WaveCtx<CAVITY>& x, double2 (&W)[5], int j, int X,
+                                           const double2& fc) {
+  double2& m = W[CFD_SLOT(X)];
+  const double2 bh = W[CFD_SLOT(X + 1)], ah = W[CFD_SLOT(X - 1)];
+#define CFD_S(b, a) ((DIR > 0) ? (b) : (a))
+#define CFD_N(b, a) ((DIR > 0) ? (a) : (b))
+  if (j > x.rmin && j < x.rmax) {  // row-uniform
+    if (((JPAR ^ COLOR) & 1) == 0) {  // slot a (even column gi) has this colour
+      const double Lb = dpp_from_left(m.y);
+      m.x = sor_fast<CAVITY>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+    } else {
+      const double Ra = dpp_from_right(m.x);
+      m.y = sor_fast<CAVITY>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+    }
+  }
+#undef CFD_S
+#undef CFD_N
+}
+
+template <int DIR, int ROT>
+__device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const double2 (&W)[5], int j, int X,
+                                             const double2& fc, bool store, double& rm) {
+  const int nx = x.g.nx, ny = x.g.ny;
+  const Coef& c = x.c;
+#define CFD_S(b, a) ((DIR > 0) ? (b) : (a))
+#define CFD_N(b, a) ((DIR > 0) ? (a) : (b))
+  if (j >= x.y0 && j < x.y1) {  // row-uniform
+    const double2 m = W[CFD_SLOT(X)], bh = W[CFD_SLOT(X + 1)], ah = W[CFD_SLOT(X - 1)];
+    const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
+    if (store && x.out_lane) {
+      double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
+#ifndef CFD_NO_NT_STORE
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      d2v mv = {m.x, m.y};
+      __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
+#else
+      *dst = m;
+#endif
+    }
+    if (j >= x.g.j0 && j <= x.g.j1) {
+      if (j == ny) {  // top row: eps_n = 0 (cavity-01.cpp:666)
+        rm = fmax(rm, fmax(residual_abs<CAVITY>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x),
+                           residual_abs<CAVITY>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y)));
+      } else {
+        rm = fmax(rm, fmax(residual_interior<CAVITY>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x),
+                           residual_interior<CAVITY>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y)));
+      }
+    }
+  }
+#undef CFD_S
+#undef CFD_N
+}
+
+template <int DIR, int ROT, int PAR, int NPR>  // PAR = parity of R
+__device__ __forceinline__ void cav_pair_step(const WaveCtx<CAVITY>& x, CavPair<NPR>& s, int R) {
+  constexpr int PD = NPR - 1;
+  s.w[CFD_SLOT(0)] = s.np[CFD_NSLOT(0)];
+  s.fr[CFD_SLOT(1)] = s.nf[CFD_NSLOT(0)];
+  s.np[CFD_NSLOT(-PD)] = x.ld_fast(x.pin, R + PD * DIR);
+  s.nf[CFD_NSLOT(-PD)] = x.ld_fast(x.f, R + (PD - 1) * DIR);
+  // iteration k: red R-d (parity PAR^1), black R-2d (PAR), residual R-3d
+  cav_update<DIR, ROT, PAR ^ 1, 0>(x, s.w, R - DIR, 1, s.fr[CFD_SLOT(1)]);
+  cav_update<DIR, ROT, PAR, 1>(x, s.w, R - 2 * DIR, 2, s.fr[CFD_SLOT(2)]);
+  cav_residual<DIR, ROT>(x, s.w, R - 3 * DIR, 3, s.fr[CFD_SLOT(3)], false, s.rmax1);
+  // iteration k+1: front row R-2d (final), red R-3d (PAR^1), black R-4d (PAR), residual + store R-5d
+  s.w2[CFD_SLOT(2)] = s.w[CFD_SLOT(2)];
+  cav_update<DIR, ROT, PAR ^ 1, 0>(x, s.w2, R - 3 * DIR, 3, s.fr[CFD_SLOT(3)]);
+  cav_update<DIR, ROT, PAR, 1>(x, s.w2, R - 4 * DIR, 4, s.fr[CFD_SLOT(4)]);
+  cav_residual<DIR, ROT>(x, s.w2, R - 5 * DIR, 5, s.fr[CFD_SLOT(5)], true, s.rmax2);
+}
+
+template <int DIR>
+__device__ __forceinline__ void wave_march_cav(const WaveCtx<CAVITY>& x, int y0, int y1, double& r1, double& r2) {
+  constexpr int H = CAV_H, NPR = CFD_PAIR_NPR;
+  const int Rb0 = (DIR > 0) ? y0 - H : y1 - 1 + H;
+  const int Rbeg = Rb0 - DIR * (Rb0 & 1);  // even first front row: compile-time colours
+  const int nsteps = (y1 - y0) + 2 * H + (Rb0 & 1);
+  CavPair<NPR> s;
+  const double2 z = make_double2(0.0, 0.0);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) s.w[k] = s.w2[k] = s.fr[k] = z;
+  s.rmax1 = s.rmax2 = 0.0;
+  {
+    constexpr int ROT = 0, PAR = 0;
+#pragma unroll
+    for (int q = 0; q < NPR - 1; ++q) {
+      s.np[CFD_NSLOT(-q)] = x.ld_fast(x.pin, Rbeg + q * DIR);
+      s.nf[CFD_NSLOT(-q)] = x.ld_fast(x.f, Rbeg + (q - 1) * DIR);
+    }
+  }
+  int R = Rbeg;
+  for (int st = 0; st < nsteps; st += 10, R += 10 * DIR) {
+    cav_pair_step<DIR, 0, 0, NPR>(x, s, R);
+    cav_pair_step<DIR, 1, 1, NPR>(x, s, R + DIR);
+    cav_pair_step<DIR, 2, 0, NPR>(x, s, R + 2 * DIR);
+    cav_pair_step<DIR, 3, 1, NPR>(x, s, R + 3 * DIR);
+    cav_pair_step<DIR, 4, 0, NPR>(x, s, R + 4 * DIR);
+    cav_pair_step<DIR, 0, 1, NPR>(x, s, R + 5 * DIR);
+    cav_pair_step<DIR, 1, 0, NPR>(x, s, R + 6 * DIR);
+    cav_pair_step<DIR, 2, 1, NPR>(x, s, R + 7 * DIR);
+    cav_pair_step<DIR, 3, 0, NPR>(x, s, R + 8 * DIR);
+    cav_pair_step<DIR, 4, 1, NPR>(x, s, R + 9 * DIR);
+  }
+  r1 = x.out_lane ? s.rmax1 : 0.0;
+  r2 = x.out_lane ? s.rmax2 : 0.0;
+}
+
 // Boundary-column waves (ghost / solid columns in the tile): general masks
 // and a 5-step unroll with the colour tested at run time - compact code, so
 // that it shares the instruction cache with the interior loops.
@@ -1619,12 +1750,22 @@ __global__ __launch_bounds__(256, CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
   const bool up = (flags & 1) && (band & 1);
   // flags bit 4 / bit 5 (timing diagnostics only): never / always take the interior path
   const bool fast = (flags & 32) || (!(flags & 16) && cols_in);
-  if (fast) {
-    if (up) wave_march_pair<CASE, -1, true>(x, y0, y1, r1, r2);
-    else wave_march_pair<CASE, 1, true>(x, y0, y1, r1, r2);
-  } else {
-    if (up) wave_march_pair_edge<CASE, -1>(x, y0, y1, r1, r2);
-    else wave_march_pair_edge<CASE, 1>(x, y0, y1, r1, r2);
+  bool done = false;
+  if constexpr (CASE == CAVITY) {
+    if (fast && !(flags & 128)) {  // flags bit 7: general pipeline instead (diagnostic)
+      if (up) wave_march_cav<-1>(x, y0, y1, r1, r2);
+      else wave_march_cav<1>(x, y0, y1, r1, r2);
+      done = true;
+    }
+  }
+  if (!done) {
+    if (fast) {
+      if (up) wave_march_pair<CASE, -1, true>(x, y0, y1, r1, r2);
+      else wave_march_pair<CASE, 1, true>(x, y0, y1, r1, r2);
+    } else {
+      if (up) wave_march_pair_edge<CASE, -1>(x, y0, y1, r1, r2);
+      else wave_march_pair_edge<CASE, 1>(x, y0, y1, r1, r2);
+    }
   }
   r1 = wave_max(r1);
   r2 = wave_max(r2);

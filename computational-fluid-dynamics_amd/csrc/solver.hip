@@ -397,9 +397,12 @@ class Solver {
     auto nbands = [](int lo, int hi, int t) { return hi > lo ? (hi - lo + t - 1) / t : 0; };
     // most interior bands whose tiles (boundary tiles included) all fit in one round
     int nb = std::max(1, std::min(waves / std::max(1, pl.ctiles), (rows + march_min_th - 1) / march_min_th));
+    // interior march: th + 2*depth + 1 rows in groups of 10 (depth 5 for the
+    // cavity's interior pipeline, 7 otherwise); boundary tiles: depth 7
+    const int lagc = (P.case_id == CFD_CAVITY) ? 11 : 15;
     for (;; --nb) {
-      pl.th = std::max(1, std::min(rmax, ((rows + nb - 1) / nb + 4) / 10 * 10 + 5));
-      pl.the = std::max(8, std::min(rmax, (pl.th + 15) * pair_edge_pct / 100 - 14));
+      pl.th = std::max(1, std::min(rmax, ((rows + nb - 1) / nb + lagc + 9) / 10 * 10 - lagc));
+      pl.the = std::max(8, std::min(rmax, (pl.th + lagc) * pair_edge_pct / 100 - 14));
       pl.nb0 = nbands(lo0, hi0, pl.th);
       pl.nb1 = nbands(lo1, hi1, pl.th);
       pl.nbe0 = nbands(lo0, hi0, pl.the);
