@@ -1469,30 +1469,32 @@ __device__ __forceinline__ void wave_march_pair(const WaveCtx<CASE>& x, int y0, 
   r2 = FAST ? (x.out_lane ? s.rmax2 : 0.0) : s.rmax2;
 }
 
-// ---- cavity interior waves: a shorter pipeline (dependency depth 5) -------
+// ---- cavity: NS red-black iterations per launch, dependency depth 2NS+1 ----
 //
 // The cavity has no ghost / solid refresh (its ghosts are fixed zeros), so a
-// row is final as soon as its black cells are updated: iteration k updates
-// red at R-1, black at R-2 and takes the residual at R-3; iteration k+1
-// takes row R-2 as its front row (red R-3, black R-4, residual + store R-5).
-// Same operations in the same order per cell as the general pipeline (bit-
-// identical); 5 halo rows instead of 7, and no final-value or second source
-// ring (fewer VGPRs).
-constexpr int CAV_H = 5;
+// row is final as soon as its black cells are updated. Sweep s of the launch
+// has front row A = R - 2s d: red at A-d, black at A-2d, residual at A-3d;
+// row A-2d, final, is the front row of sweep s+1; the last sweep also stores.
+// Same operations in the same order per cell as one launch per iteration, so
+// the result is bit-identical. NS = 2: 5 halo rows; NS = 3: 7 (the 8-column
+// halos of PAIR_TWC fit both). Interior-column waves use the unmasked forms
+// (sor_fast / residual_interior, rows by uniform branches); boundary-column
+// waves the reference's masked forms (sor_update / residual_abs).
 
-template <int NPR>
-struct CavPair {
-  double2 w[5];    // iteration k (final after black), rows R-4d .. R
-  double2 w2[5];   // iteration k+1, rows R-6d .. R-2d
-  double2 fr[5];   // source rows R-d .. R-5d
-  double2 np[NPR]; // prefetched p_in rows R .. R+(NPR-1)d
-  double2 nf[NPR]; // prefetched f rows R-d .. R+(NPR-2)d
-  double rmax1, rmax2;
+template <int NS>
+struct CavRun {
+  double2 w[NS][5];  // sweep s: rows R-2s d .. R-(2s+4) d
+  double2 fr[10];    // source rows R-d .. R-10d
+  double2 np[5];     // prefetched p_in rows R .. R+4d
+  double2 nf[5];     // prefetched f rows R-d .. R+3d
+  double rmax[NS];
 };
 
-// red (COLOR 0) / black (COLOR 1) update of row j = R - X*d on a ring; j's
-// parity is JPAR (compile time)
-template <int DIR, int ROT, int JPAR, int COLOR>
+// slot of row R - X d in a 10-slot ring at step t = (ROT, PAR) of the 10-step march
+#define CFD_S10(X) ((((6 * (ROT) + 5 * (PAR)) % 10 + 9 - (X)) % 10 + 20) % 10)
+
+// red (COLOR 0) / black (COLOR 1) update of row j = R - X d (parity JPAR)
+template <int DIR, int ROT, int JPAR, int COLOR, bool EDGE>
 __device__ __forceinline__ void cav_update(const WaveCtx<CAVITY>& x, double2 (&W)[5], int j, int X,
                                            const double2& fc) {
   double2& m = W[CFD_SLOT(X)];
@@ -1502,17 +1504,29 @@ __device__ __forceinline__ void cav_update(const WaveCtx<CAVITY>& x, double2 (&W
   if (j > x.rmin && j < x.rmax) {  // row-uniform
     if (((JPAR ^ COLOR) & 1) == 0) {  // slot a (even column gi) has this colour
       const double Lb = dpp_from_left(m.y);
-      m.x = sor_fast<CAVITY>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+      if (EDGE) {
+        const double nv = sor_update<CAVITY>(x.c, x.g.nx, x.g.ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x),
+                                             CFD_N(bh.x, ah.x), fc.x);
+        m.x = x.fl_a(j) ? nv : m.x;
+      } else {
+        m.x = sor_fast<CAVITY>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+      }
     } else {
       const double Ra = dpp_from_right(m.x);
-      m.y = sor_fast<CAVITY>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+      if (EDGE) {
+        const double nv = sor_update<CAVITY>(x.c, x.g.nx, x.g.ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y),
+                                             CFD_N(bh.y, ah.y), fc.y);
+        m.y = x.fl_b(j) ? nv : m.y;
+      } else {
+        m.y = sor_fast<CAVITY>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+      }
     }
   }
 #undef CFD_S
 #undef CFD_N
 }
 
-template <int DIR, int ROT>
+template <int DIR, int ROT, bool EDGE>
 __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const double2 (&W)[5], int j, int X,
                                              const double2& fc, bool store, double& rm) {
   const int nx = x.g.nx, ny = x.g.ny;
@@ -1527,16 +1541,23 @@ __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const dou
 #ifndef CFD_NO_NT_STORE
       typedef double d2v __attribute__((ext_vector_type(2)));
       d2v mv = {m.x, m.y};
-      __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
+      __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));  // streamed: keep L2 for re-read halo rows
 #else
       *dst = m;
 #endif
     }
     if (j >= x.g.j0 && j <= x.g.j1) {
-      if (j == ny) {  // top row: eps_n = 0 (cavity-01.cpp:666)
+      if (EDGE) {
+        const double ra = residual_abs<CAVITY>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+        const double rb =
+            residual_abs<CAVITY>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+        rm = fmax(rm, (x.out_lane && x.fl_a(j)) ? ra : 0.0);
+        rm = fmax(rm, (x.out_lane && x.fl_b(j)) ? rb : 0.0);
+      } else if (j == ny) {  // top row: eps_n = 0 (cavity-01.cpp:666)
         rm = fmax(rm, fmax(residual_abs<CAVITY>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x),
                            residual_abs<CAVITY>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y)));
       } else {
+        // both cells first: one max per row touches the loop-carried accumulator
         rm = fmax(rm, fmax(residual_interior<CAVITY>(c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x),
                            residual_interior<CAVITY>(c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y)));
       }
@@ -1546,59 +1567,75 @@ __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const dou
 #undef CFD_N
 }
 
-template <int DIR, int ROT, int PAR, int NPR>  // PAR = parity of R
-__device__ __forceinline__ void cav_pair_step(const WaveCtx<CAVITY>& x, CavPair<NPR>& s, int R) {
-  constexpr int PD = NPR - 1;
-  s.w[CFD_SLOT(0)] = s.np[CFD_NSLOT(0)];
-  s.fr[CFD_SLOT(1)] = s.nf[CFD_NSLOT(0)];
-  s.np[CFD_NSLOT(-PD)] = x.ld_fast(x.pin, R + PD * DIR);
-  s.nf[CFD_NSLOT(-PD)] = x.ld_fast(x.f, R + (PD - 1) * DIR);
-  // iteration k: red R-d (parity PAR^1), black R-2d (PAR), residual R-3d
-  cav_update<DIR, ROT, PAR ^ 1, 0>(x, s.w, R - DIR, 1, s.fr[CFD_SLOT(1)]);
-  cav_update<DIR, ROT, PAR, 1>(x, s.w, R - 2 * DIR, 2, s.fr[CFD_SLOT(2)]);
-  cav_residual<DIR, ROT>(x, s.w, R - 3 * DIR, 3, s.fr[CFD_SLOT(3)], false, s.rmax1);
-  // iteration k+1: front row R-2d (final), red R-3d (PAR^1), black R-4d (PAR), residual + store R-5d
-  s.w2[CFD_SLOT(2)] = s.w[CFD_SLOT(2)];
-  cav_update<DIR, ROT, PAR ^ 1, 0>(x, s.w2, R - 3 * DIR, 3, s.fr[CFD_SLOT(3)]);
-  cav_update<DIR, ROT, PAR, 1>(x, s.w2, R - 4 * DIR, 4, s.fr[CFD_SLOT(4)]);
-  cav_residual<DIR, ROT>(x, s.w2, R - 5 * DIR, 5, s.fr[CFD_SLOT(5)], true, s.rmax2);
+// sweeps S .. NS-1 of one march step (compile-time recursion over the sweeps)
+template <int S, int NS, int DIR, int ROT, int PAR, bool EDGE>
+__device__ __forceinline__ void cav_sweeps(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R) {
+  if constexpr (S < NS) {
+    // red at R-(2S+1)d (parity PAR^1), black at R-(2S+2)d (PAR), residual at R-(2S+3)d
+    cav_update<DIR, ROT, PAR ^ 1, 0, EDGE>(x, s.w[S], R - (2 * S + 1) * DIR, 2 * S + 1, s.fr[CFD_S10(2 * S + 1)]);
+    cav_update<DIR, ROT, PAR, 1, EDGE>(x, s.w[S], R - (2 * S + 2) * DIR, 2 * S + 2, s.fr[CFD_S10(2 * S + 2)]);
+    cav_residual<DIR, ROT, EDGE>(x, s.w[S], R - (2 * S + 3) * DIR, 2 * S + 3, s.fr[CFD_S10(2 * S + 3)], S == NS - 1,
+                                 s.rmax[S]);
+    if constexpr (S + 1 < NS) s.w[S + 1][CFD_SLOT(2 * S + 2)] = s.w[S][CFD_SLOT(2 * S + 2)];
+    cav_sweeps<S + 1, NS, DIR, ROT, PAR, EDGE>(x, s, R);
+  }
 }
 
-template <int DIR>
-__device__ __forceinline__ void wave_march_cav(const WaveCtx<CAVITY>& x, int y0, int y1, double& r1, double& r2) {
-  constexpr int H = CAV_H, NPR = CFD_PAIR_NPR;
+template <int NS, int DIR, int ROT, int PAR, bool EDGE>  // PAR = parity of R
+__device__ __forceinline__ void cav_step(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R) {
+  s.w[0][CFD_SLOT(0)] = s.np[CFD_SLOT(0)];
+  s.fr[CFD_S10(1)] = s.nf[CFD_SLOT(0)];
+  if (EDGE) {
+    s.np[CFD_SLOT(-4)] = x.ld(x.pin, R + 4 * DIR);
+    s.nf[CFD_SLOT(-4)] = x.ld(x.f, R + 3 * DIR);
+  } else {
+    s.np[CFD_SLOT(-4)] = x.ld_fast(x.pin, R + 4 * DIR);
+    s.nf[CFD_SLOT(-4)] = x.ld_fast(x.f, R + 3 * DIR);
+  }
+  cav_sweeps<0, NS, DIR, ROT, PAR, EDGE>(x, s, R);
+}
+
+template <int NS, int DIR, bool EDGE>
+__device__ __forceinline__ void cav_march(const WaveCtx<CAVITY>& x, int y0, int y1, double (&r)[NS]) {
+  constexpr int H = 2 * NS + 1;
   const int Rb0 = (DIR > 0) ? y0 - H : y1 - 1 + H;
   const int Rbeg = Rb0 - DIR * (Rb0 & 1);  // even first front row: compile-time colours
   const int nsteps = (y1 - y0) + 2 * H + (Rb0 & 1);
-  CavPair<NPR> s;
+  CavRun<NS> s;
   const double2 z = make_double2(0.0, 0.0);
 #pragma unroll
-  for (int k = 0; k < 5; ++k) s.w[k] = s.w2[k] = s.fr[k] = z;
-  s.rmax1 = s.rmax2 = 0.0;
-  {
-    constexpr int ROT = 0, PAR = 0;
+  for (int k = 0; k < 5; ++k)
 #pragma unroll
-    for (int q = 0; q < NPR - 1; ++q) {
-      s.np[CFD_NSLOT(-q)] = x.ld_fast(x.pin, Rbeg + q * DIR);
-      s.nf[CFD_NSLOT(-q)] = x.ld_fast(x.f, Rbeg + (q - 1) * DIR);
+    for (int q = 0; q < NS; ++q) s.w[q][k] = z;
+#pragma unroll
+  for (int k = 0; k < 10; ++k) s.fr[k] = z;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) s.rmax[q] = 0.0;
+  {
+    constexpr int ROT = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s.np[CFD_SLOT(-q)] = EDGE ? x.ld(x.pin, Rbeg + q * DIR) : x.ld_fast(x.pin, Rbeg + q * DIR);
+      s.nf[CFD_SLOT(-q)] = EDGE ? x.ld(x.f, Rbeg + (q - 1) * DIR) : x.ld_fast(x.f, Rbeg + (q - 1) * DIR);
     }
   }
   int R = Rbeg;
   for (int st = 0; st < nsteps; st += 10, R += 10 * DIR) {
-    cav_pair_step<DIR, 0, 0, NPR>(x, s, R);
-    cav_pair_step<DIR, 1, 1, NPR>(x, s, R + DIR);
-    cav_pair_step<DIR, 2, 0, NPR>(x, s, R + 2 * DIR);
-    cav_pair_step<DIR, 3, 1, NPR>(x, s, R + 3 * DIR);
-    cav_pair_step<DIR, 4, 0, NPR>(x, s, R + 4 * DIR);
-    cav_pair_step<DIR, 0, 1, NPR>(x, s, R + 5 * DIR);
-    cav_pair_step<DIR, 1, 0, NPR>(x, s, R + 6 * DIR);
-    cav_pair_step<DIR, 2, 1, NPR>(x, s, R + 7 * DIR);
-    cav_pair_step<DIR, 3, 0, NPR>(x, s, R + 8 * DIR);
-    cav_pair_step<DIR, 4, 1, NPR>(x, s, R + 9 * DIR);
+    cav_step<NS, DIR, 0, 0, EDGE>(x, s, R);
+    cav_step<NS, DIR, 1, 1, EDGE>(x, s, R + DIR);
+    cav_step<NS, DIR, 2, 0, EDGE>(x, s, R + 2 * DIR);
+    cav_step<NS, DIR, 3, 1, EDGE>(x, s, R + 3 * DIR);
+    cav_step<NS, DIR, 4, 0, EDGE>(x, s, R + 4 * DIR);
+    cav_step<NS, DIR, 0, 1, EDGE>(x, s, R + 5 * DIR);
+    cav_step<NS, DIR, 1, 0, EDGE>(x, s, R + 6 * DIR);
+    cav_step<NS, DIR, 2, 1, EDGE>(x, s, R + 7 * DIR);
+    cav_step<NS, DIR, 3, 0, EDGE>(x, s, R + 8 * DIR);
+    cav_step<NS, DIR, 4, 1, EDGE>(x, s, R + 9 * DIR);
   }
-  r1 = x.out_lane ? s.rmax1 : 0.0;
-  r2 = x.out_lane ? s.rmax2 : 0.0;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) r[q] = (EDGE || x.out_lane) ? s.rmax[q] : 0.0;
 }
+#undef CFD_S10
 
 // Boundary-column waves (ghost / solid columns in the tile): general masks
 // and a 5-step unroll with the colour tested at run time - compact code, so
@@ -1644,6 +1681,9 @@ __device__ __forceinline__ void wave_march_pair_edge(const WaveCtx<CASE>& x, int
 #ifndef CFD_PAIR_MIN_WAVES
 #define CFD_PAIR_MIN_WAVES 2
 #endif
+#ifndef CFD_CAV_MIN_WAVES
+#define CFD_CAV_MIN_WAVES 3  // the cavity pair kernel fits 3 waves/SIMD with room (129 VGPRs)
+#endif
 
 // Tiling of one pair launch. Rows are covered in up to two ranges [lo0, hi0)
 // and [lo1, hi1) (the second may be empty): one launch for a whole strip, or,
@@ -1659,7 +1699,7 @@ struct PairPlan {
 };
 
 template <int CASE>
-__global__ __launch_bounds__(256, CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
+__global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
     Geo g, Coef c, const double* __restrict__ pin, double* __restrict__ pout, const double* __restrict__ f,
     PoissonCtl ctl, int k, int lag, PairPlan pl, int flags) {
   // tiles: the first and last column tile (boundary columns, general masks)
@@ -1750,15 +1790,14 @@ __global__ __launch_bounds__(256, CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
   const bool up = (flags & 1) && (band & 1);
   // flags bit 4 / bit 5 (timing diagnostics only): never / always take the interior path
   const bool fast = (flags & 32) || (!(flags & 16) && cols_in);
-  bool done = false;
-  if constexpr (CASE == CAVITY) {
-    if (fast && !(flags & 128)) {  // flags bit 7: general pipeline instead (diagnostic)
-      if (up) wave_march_cav<-1>(x, y0, y1, r1, r2);
-      else wave_march_cav<1>(x, y0, y1, r1, r2);
-      done = true;
-    }
-  }
-  if (!done) {
+  if constexpr (CASE == CAVITY) {  // the cavity's own depth-5 pipeline (no refresh stage)
+    double r[2];
+    if (!fast) cav_march<2, 1, true>(x, y0, y1, r);
+    else if (up) cav_march<2, -1, false>(x, y0, y1, r);
+    else cav_march<2, 1, false>(x, y0, y1, r);
+    r1 = r[0];
+    r2 = r[1];
+  } else {
     if (fast) {
       if (up) wave_march_pair<CASE, -1, true>(x, y0, y1, r1, r2);
       else wave_march_pair<CASE, 1, true>(x, y0, y1, r1, r2);
