@@ -25,7 +25,7 @@ constexpr int CAVITY = 0, CHANNEL = 1, BACKSTEP = 2;
 constexpr int HALO = 8;           // halo rows stored per side (a fused pair of SOR iterations needs 7)
 constexpr int RES_SHARDS = 32;    // residual / max accumulators, one 128-B line each
 constexpr int SHARD_STRIDE = 16;  // doubles between shards (128 B)
-constexpr int RING = 8;           // residual ring slots (iteration k uses k & 7)
+constexpr int RING = 16;          // residual ring slots (iteration k uses k & 15)
 
 struct Geo {
   int nx, ny;      // global interior cells
@@ -1129,50 +1129,38 @@ __device__ __forceinline__ bool pair_go_on(const PoissonCtl& ctl, int kk, int la
   return prev > tol;
 }
 
+// The reference's while condition for the iterations [ka, kb] the host gave
+// this launch (the previous launch's, or with the lagged test the one before;
+// 0 = the initial residual; others only on check_every multiples): the first
+// one that meets the tolerance ends the solve there. Returns false if this
+// launch has nothing to do (stopped now or earlier). All waves agree.
+__device__ __forceinline__ bool window_go_on(const PoissonCtl& ctl, int ka, int kb, int lane, bool first_wave) {
+  if (ctl.stop[0] != 0) return false;
+  const double tol = ctl.tol[0];
+  for (int kk = ka; kk <= kb; ++kk) {
+    if (!(kk == 0 || (kk >= 1 && kk % ctl.check_every == 0))) continue;
+    if (!pair_go_on(ctl, kk, lane, tol)) {
+      if (first_wave && lane == 0) {
+        ctl.stop[1] = kk;
+        ctl.stop[0] = 1;
+      }
+      return false;
+    }
+  }
+  return true;
+}
+
 template <int CASE>
 __global__ __launch_bounds__(256, CFD_WAVE_MIN_WAVES) void poisson_wave_kernel(Geo g, Coef c, const double* __restrict__ pin,
                                                            double* __restrict__ pout, const double* __restrict__ f,
-                                                           PoissonCtl ctl, int k, int TH, int ctiles, int nbands,
-                                                           int flags) {
+                                                           PoissonCtl ctl, int k, int ka, int kb, int TH, int ctiles,
+                                                           int nbands, int flags) {
   constexpr int H = 4, TWC = 128 - 2 * H;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // convergence test of the iterations [ka, kb] (flags bit 2: none - a replay
+  // of an iteration already known to be the solve's last)
+  if (!(flags & 4) && !window_go_on(ctl, ka, kb, lane, blockIdx.x == 0 && wv == 0)) return;
 
-  // convergence test of the previous iteration, per wave (all waves agree);
-  // flags bit 2 = replay of an iteration already known to be the last one
-  if (!(flags & 4)) {
-    const double tol = ctl.tol[0];
-    const bool stopped = ctl.stop[0] != 0;
-    const bool check = (k == 1) || ((k - 1) % ctl.check_every == 0);
-    bool active;
-    if (stopped) {
-      active = false;
-    } else if ((flags & 8) && k >= 3 && (k - 2) % ctl.check_every == 0 && !pair_go_on(ctl, k - 2, lane, tol)) {
-      // flags bit 3: the previous launch was a pair, whose first iteration
-      // (k-2) no launch has tested yet
-      active = false;
-      if (lane == 0 && wv == 0 && blockIdx.x == 0) {
-        ctl.stop[1] = k - 2;
-        ctl.stop[0] = 1;
-      }
-    } else if (!check) {
-      active = true;
-    } else {
-      double prev;
-      if (k == 1) {
-        prev = ctl.tol[1];
-      } else {
-        const double* slot = ctl.ring + (size_t)((k - 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-        prev = (lane < RES_SHARDS) ? slot[lane * SHARD_STRIDE] : 0.0;
-        prev = wave_max(prev);
-      }
-      active = prev > tol;
-      if (!active && lane == 0 && wv == 0 && blockIdx.x == 0) {
-        ctl.stop[1] = k - 1;
-        ctl.stop[0] = 1;
-      }
-    }
-    if (!active) return;
-  }
   if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS)
     ctl.ring[(size_t)((k + 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
 
@@ -1698,10 +1686,12 @@ struct PairPlan {
   int lo0, hi0, lo1, hi1;
 };
 
-template <int CASE>
-__global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAIR_MIN_WAVES) void poisson_pair_kernel(
+template <int CASE, int NS>
+__global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAIR_MIN_WAVES) void poisson_multi_kernel(
     Geo g, Coef c, const double* __restrict__ pin, double* __restrict__ pout, const double* __restrict__ f,
-    PoissonCtl ctl, int k, int lag, PairPlan pl, int flags) {
+    PoissonCtl ctl, int k, int ka, int kb, PairPlan pl, int flags) {
+  // NS red-black iterations k .. k+NS-1 in one launch (NS = 3: cavity only)
+  static_assert(NS == 2 || (NS == 3 && CASE == CAVITY), "three sweeps per launch: cavity pipeline only");
   // tiles: the first and last column tile (boundary columns, general masks)
   // in bands of pl.the rows, then the interior column tiles in bands of pl.th
   // rows; the host makes the boundary bands shorter so that their slower
@@ -1710,29 +1700,12 @@ __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAI
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: band / row logic stays scalar
 
-  // convergence tests of the previous pair's iterations k-2, k-1 (lag 1: of
-  // the pair before, k-4, k-3; iteration 0 = the initial residual), all waves
-  // agree: the first that meets the tolerance (on a tested iteration) ends the
-  // solve there
-  {
-    const double tol = ctl.tol[0];
-    if (ctl.stop[0] != 0) return;
-    int stop_at = -1;
-    const int ka = k - 2 - 2 * lag, kb = k - 1 - 2 * lag;
-    auto tested = [&](int kk) { return kk == 0 || (kk >= 1 && kk % ctl.check_every == 0); };
-    if (tested(ka) && !pair_go_on(ctl, ka, lane, tol)) stop_at = ka;
-    else if (tested(kb) && !pair_go_on(ctl, kb, lane, tol)) stop_at = kb;
-    if (stop_at >= 0) {
-      if (lane == 0 && wv == 0 && blockIdx.x == 0) {
-        ctl.stop[1] = stop_at;
-        ctl.stop[0] = 1;
-      }
-      return;
-    }
-  }
-  if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS) {
-    ctl.ring[(size_t)((k + 2) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
-    ctl.ring[(size_t)((k + 3) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
+  // convergence test of the iterations [ka, kb] (flags bit 2: none, a replay)
+  if (!(flags & 4) && !window_go_on(ctl, ka, kb, lane, blockIdx.x == 0 && wv == 0)) return;
+  if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS) {  // the next launch's residual slots
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+      ctl.ring[(size_t)((k + NS + q) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
   }
 
   const int nblk = (int)gridDim.x;
@@ -1786,18 +1759,16 @@ __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAI
   // neighbours (rows are handled row-uniformly inside the fast march)
   const int c0 = ctile * PAIR_TWC - H;
   const bool cols_in = c0 >= 1 && c0 + 127 <= g.nx && (CASE != BACKSTEP || c0 > c.step_i + 1);
-  double r1 = 0.0, r2 = 0.0;
   const bool up = (flags & 1) && (band & 1);
   // flags bit 4 / bit 5 (timing diagnostics only): never / always take the interior path
   const bool fast = (flags & 32) || (!(flags & 16) && cols_in);
-  if constexpr (CASE == CAVITY) {  // the cavity's own depth-5 pipeline (no refresh stage)
-    double r[2];
-    if (!fast) cav_march<2, 1, true>(x, y0, y1, r);
-    else if (up) cav_march<2, -1, false>(x, y0, y1, r);
-    else cav_march<2, 1, false>(x, y0, y1, r);
-    r1 = r[0];
-    r2 = r[1];
+  double r[NS];
+  if constexpr (CASE == CAVITY) {  // the cavity's own pipeline (no refresh stage: depth 2NS+1)
+    if (!fast) cav_march<NS, 1, true>(x, y0, y1, r);
+    else if (up) cav_march<NS, -1, false>(x, y0, y1, r);
+    else cav_march<NS, 1, false>(x, y0, y1, r);
   } else {
+    double r1 = 0.0, r2 = 0.0;
     if (fast) {
       if (up) wave_march_pair<CASE, -1, true>(x, y0, y1, r1, r2);
       else wave_march_pair<CASE, 1, true>(x, y0, y1, r1, r2);
@@ -1805,16 +1776,18 @@ __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAI
       if (up) wave_march_pair_edge<CASE, -1>(x, y0, y1, r1, r2);
       else wave_march_pair_edge<CASE, 1>(x, y0, y1, r1, r2);
     }
+    r[0] = r1;
+    r[NS - 1] = r2;
   }
-  r1 = wave_max(r1);
-  r2 = wave_max(r2);
+#pragma unroll
+  for (int q = 0; q < NS; ++q) r[q] = wave_max(r[q]);
   if (lane == 0) {
-    double* s1 = ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-    double* s2 = ctl.ring + (size_t)((k + 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-    atomicMax(reinterpret_cast<unsigned long long*>(s1 + (size_t)(tile % RES_SHARDS) * SHARD_STRIDE),
-              (unsigned long long)__double_as_longlong(r1));
-    atomicMax(reinterpret_cast<unsigned long long*>(s2 + (size_t)(tile % RES_SHARDS) * SHARD_STRIDE),
-              (unsigned long long)__double_as_longlong(r2));
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      double* sl = ctl.ring + (size_t)((k + q) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+      atomicMax(reinterpret_cast<unsigned long long*>(sl + (size_t)(tile % RES_SHARDS) * SHARD_STRIDE),
+                (unsigned long long)__double_as_longlong(r[q]));
+    }
   }
 }
 

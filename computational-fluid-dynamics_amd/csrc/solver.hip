@@ -107,7 +107,26 @@ class Solver {
   // residuals of pair m-2, whose all-reduce then runs beside launch m-1
   // instead of in front of launch m. A third pressure buffer keeps the input
   // and output of the pair a late stop lands in intact.
-  bool lagged() const { return overlap && P.sweeps_per_launch != 1 && kernel_variant == 0; }
+  bool lagged() const { return overlap && sweeps_per_launch() >= 2; }
+  // red-black iterations per SOR launch: 3 for the cavity (its depth-7
+  // pipeline fits the 8-row halos), 2 for the open cases, 1 on request or for
+  // the legacy kernel variants
+  int sweeps_per_launch() const {
+    if (kernel_variant != 0 || P.sweeps_per_launch == 1) return 1;
+    if (P.sweeps_per_launch == 2) return 2;
+    return P.case_id == CFD_CAVITY ? 3 : 2;
+  }
+  struct LaunchRec {
+    int first, n;  // iterations first .. first+n-1
+  };
+  std::vector<LaunchRec> launches;  // SOR launches of the current solve
+  LaunchRec ar_pending{0, 0};       // overlapped launch whose residual all-reduce is not enqueued yet
+
+  // enqueue the pending (lagged) all-reduce of an overlapped launch on xs
+  void flush_allreduce(hipStream_t xs) {
+    if (ar_pending.n > 0) allreduce_slots(ar_pending.first, ar_pending.n, xs);
+    ar_pending = {0, 0};
+  }
   int nbufs() const { return lagged() ? 3 : 2; }
   bool b_pending = false;   // st_b has work that st has not waited for yet
   int last_bnd = 0;         // ev_bnd slot recorded last
@@ -147,7 +166,12 @@ class Solver {
       if (const char* e = std::getenv("CFD_WAVE_WPS")) wps = std::max(1, std::atoi(e));
       resident_waves = wps * 4 * prop.multiProcessorCount;
       int pps = 0;
-      HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pps, poisson_pair_kernel<CAVITY>, 256, 0));
+      if (P.case_id == CFD_CAVITY)  // resident waves of the launch the solve runs most
+        HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pps, poisson_multi_kernel<CAVITY, 3>, 256, 0));
+      else if (P.case_id == CFD_CHANNEL)
+        HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pps, poisson_multi_kernel<CHANNEL, 2>, 256, 0));
+      else
+        HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pps, poisson_multi_kernel<BACKSTEP, 2>, 256, 0));
       pps = std::max(1, std::min(pps, 4));
       if (const char* e = std::getenv("CFD_PAIR_WPS")) pps = std::max(1, std::atoi(e));
       if (const char* e = std::getenv("CFD_PAIR_EDGE_PCT")) pair_edge_pct = std::max(10, std::min(100, std::atoi(e)));
@@ -249,7 +273,9 @@ class Solver {
     if (!(P.omega > 0) || !(P.omega < 2)) throw Error(CFD_E_ARG, "SOR omega must lie in (0, 2)");
     if (P.max_iters < 0) throw Error(CFD_E_ARG, "max_iters must be >= 0");
     if (P.check_every < 1) throw Error(CFD_E_ARG, "check_every must be >= 1");
-    if (P.sweeps_per_launch < 0 || P.sweeps_per_launch > 2) throw Error(CFD_E_ARG, "sweeps_per_launch must be 0, 1 or 2");
+    if (P.sweeps_per_launch < 0 || P.sweeps_per_launch > 3) throw Error(CFD_E_ARG, "sweeps_per_launch must be 0, 1, 2 or 3");
+    if (P.sweeps_per_launch == 3 && P.case_id != CFD_CAVITY)
+      throw Error(CFD_E_ARG, "three sweeps per launch are implemented for the cavity only");
     if (P.ordering != CFD_ORDER_RB && P.ordering != CFD_ORDER_LEX) throw Error(CFD_E_ARG, "unknown ordering");
     if (P.ordering == CFD_ORDER_LEX && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
       throw Error(CFD_E_ARG, "lexicographic ordering supports nx + ny < 12000");
@@ -381,28 +407,29 @@ class Solver {
     nbands = (rows + th - 1) / th;
   }
 
-  // Tiling of a pair launch over rows [lo0, hi0) + [lo1, hi1) with about
+  // Rows one interior wave marches beyond its band (both sides together, plus
+  // the parity alignment row) for an n-sweep launch: the cavity's pipeline has
+  // depth 2n+1, the open cases' pair pipeline 7.
+  int march_extra(int n) const { return (P.case_id == CFD_CAVITY) ? 2 * (2 * n + 1) + 1 : 15; }
+
+  // Tiling of an n-sweep launch over rows [lo0, hi0) + [lo1, hi1) with at most
   // `waves` waves (one resident round). Interior column tiles: bands of th
-  // rows; the pair kernel marches in groups of 10 rows over th + 15 rows
-  // (th + 14 + parity alignment), so th = 5 mod 10 wastes no group. The two
-  // boundary column tiles march slower (masks): shorter bands, pair_edge_pct %
-  // of the interior march length.
-  PairPlan pair_plan(int lo0, int hi0, int lo1, int hi1, int waves) const {
+  // rows, marched in groups of 10 over th + march_extra rows, so th + extra is
+  // a multiple of 10. The two boundary column tiles march slower (masks):
+  // shorter bands, pair_edge_pct % of the interior march.
+  PairPlan multi_plan(int lo0, int hi0, int lo1, int hi1, int waves, int n) const {
     PairPlan pl{};
     pl.ctiles = (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC;
     pl.lo0 = lo0; pl.hi0 = hi0; pl.lo1 = lo1; pl.hi1 = hi1;
     const int rows = (hi0 - lo0) + (hi1 - lo1);
     const int ne = pl.ctiles >= 2 ? 2 : 1;
     const int rmax = std::max(hi0 - lo0, hi1 - lo1);
+    const int ex = march_extra(n);
     auto nbands = [](int lo, int hi, int t) { return hi > lo ? (hi - lo + t - 1) / t : 0; };
-    // most interior bands whose tiles (boundary tiles included) all fit in one round
     int nb = std::max(1, std::min(waves / std::max(1, pl.ctiles), (rows + march_min_th - 1) / march_min_th));
-    // interior march: th + 2*depth + 1 rows in groups of 10 (depth 5 for the
-    // cavity's interior pipeline, 7 otherwise); boundary tiles: depth 7
-    const int lagc = (P.case_id == CFD_CAVITY) ? 11 : 15;
-    for (;; --nb) {
-      pl.th = std::max(1, std::min(rmax, ((rows + nb - 1) / nb + lagc + 9) / 10 * 10 - lagc));
-      pl.the = std::max(8, std::min(rmax, (pl.th + lagc) * pair_edge_pct / 100 - 14));
+    for (;; --nb) {  // most interior bands whose tiles (boundary tiles included) fit one round
+      pl.th = std::max(1, std::min(rmax, ((rows + nb - 1) / nb + ex + 9) / 10 * 10 - ex));
+      pl.the = std::max(8, std::min(rmax, (pl.th + ex) * pair_edge_pct / 100 - ex));
       pl.nb0 = nbands(lo0, hi0, pl.th);
       pl.nb1 = nbands(lo1, hi1, pl.th);
       pl.nbe0 = nbands(lo0, hi0, pl.the);
@@ -413,32 +440,40 @@ class Solver {
     return pl;
   }
 
+  // One launch of poisson_multi_kernel: iterations k .. k+n-1 (n = 2, or 3 for
+  // the cavity), testing iterations [ka, kb] first (empty: ka > kb).
   template <int CASE>
-  void launch_pair(const PairPlan& pl, const Geo& g, const double* pin, double* pout, const double* f,
-                   const PoissonCtl& ctl, int k, hipStream_t stream, int lag = 0) {
+  void launch_multi(int n, const PairPlan& pl, const Geo& g, const double* pin, double* pout, const double* f,
+                    const PoissonCtl& ctl, int k, int ka, int kb, hipStream_t stream, bool replay = false) {
+    const int fl = march_flags | (replay ? 4 : 0);  // bit 2: no test at all (the solve has already stopped)
     const int ne = pl.ctiles >= 2 ? 2 : 1;
     const int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
     if (ntiles == 0) return;
-    poisson_pair_kernel<CASE><<<(ntiles + 3) / 4, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, lag, pl,
-                                                                    march_flags);
+    const dim3 grid((ntiles + 3) / 4);
+    if constexpr (CASE == CAVITY) {
+      if (n == 3) {
+        poisson_multi_kernel<CASE, 3><<<grid, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, ka, kb, pl, fl);
+        return;
+      }
+    }
+    poisson_multi_kernel<CASE, 2><<<grid, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, ka, kb, pl, fl);
   }
 
-  // One SOR launch: iteration k (sweeps == 1) or iterations k, k+1 (sweeps == 2).
-  // replay: iteration k is already known to be the solve's last (no test).
+  // One SOR launch over every strip: iterations k .. k+n-1, testing [ka, kb].
   template <int CASE>
-  void launch_poisson(const double* const* pin, double* const* pout, int k, int sweeps, bool replay, bool after_pair) {
+  void launch_poisson(const double* const* pin, double* const* pout, int k, int n, int ka, int kb, bool replay) {
     PoissonCtl ctl{ring, tolv, stop, P.check_every};
     for (size_t q = 0; q < S.size(); ++q) {
       const Geo& g = S[q].g;
       const int rows = g.wj1 - g.wj0 + 1;
       int ctiles, th, nbands;
-      if (sweeps == 2) {
-        const PairPlan pl = pair_plan(g.wj0, g.wj1 + 1, 0, 0, resident_pair_waves / (int)S.size());
-        launch_pair<CASE>(pl, g, pin[q], pout[q], S[q].b[B_F], ctl, k, st);
-      } else if (kernel_variant == 1 && !replay) {
+      if (n >= 2) {
+        const PairPlan pl = multi_plan(g.wj0, g.wj1 + 1, 0, 0, resident_pair_waves / (int)S.size(), n);
+        launch_multi<CASE>(n, pl, g, pin[q], pout[q], S[q].b[B_F], ctl, k, ka, kb, st, replay);
+      } else if (kernel_variant == 1) {  // legacy variants (one sweep per launch only): test k-1 themselves
         const dim3 grid((P.nx + 2 + PBX - 1) / PBX, (rows + PBY - 1) / PBY);
         poisson_rbsor_kernel<CASE, PBX, PBY><<<grid, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k);
-      } else if (kernel_variant == 2 && !replay) {
+      } else if (kernel_variant == 2) {
         constexpr int TW = 256 - 8;
         // one resident round: split each column tile's rows evenly over the
         // blocks the device holds at once (no tail of a second, partial round)
@@ -448,15 +483,13 @@ class Solver {
       } else {
         wave_bands(rows, 128 - 8, resident_waves, ctiles, th, nbands);
         const int nblk = (ctiles * nbands + 3) / 4;
-        poisson_wave_kernel<CASE><<<nblk, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k, th, ctiles,
-                                                         nbands, march_flags | (replay ? 4 : 0) | (after_pair ? 8 : 0));
+        poisson_wave_kernel<CASE><<<nblk, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k, ka, kb, th, ctiles,
+                                                         nbands, march_flags | (replay ? 4 : 0));
       }
     }
     check_launch("poisson");
   }
 
-  // SOR launch number m (0-based) of a solve starting in buffer `base`: reads
-  // buffer (base+m)&1, writes the other. Iterations k .. k+sweeps-1.
   // st waits for everything enqueued on st_b so far
   void join_b() {
     if (b_pending) {
@@ -465,14 +498,9 @@ class Solver {
     }
   }
 
-  // Pair launch m on a rank with halo overlap. st_b: exchange of launch m's
-  // input rows, then the rows within OVL_ROWS of each neighbour (their cone
-  // reaches the interior rows of launch m-1: wait for it); st: the interior
-  // rows (they never read halo rows; wait for launch m-1's boundary rows).
-  // The residual all-reduce of the pair follows both, on st_b.
-  // all-reduce (max) of the residual slots of iterations k, k+1 that are tested
-  void allreduce_pair_slots(int k, hipStream_t xs) {
-    for (int kk = k; kk < k + 2 && kk <= P.max_iters; ++kk) {
+  // all-reduce (max) of the residual slots of iterations k .. k+n-1 that are tested
+  void allreduce_slots(int k, int n, hipStream_t xs) {
+    for (int kk = k; kk < k + n && kk <= P.max_iters; ++kk) {
       if (kk % P.check_every == 0 || kk == P.max_iters) {
         double* slot = ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
         comm_allreduce_max(comm, slot, RES_SHARDS * SHARD_STRIDE, xs);
@@ -480,8 +508,14 @@ class Solver {
     }
   }
 
+  // Launch m (n >= 2 sweeps) on a rank with halo overlap. st_b: exchange of
+  // the launch's input rows, the all-reduce of launch m-1's residuals (tested
+  // by launch m+1: lagged), then the rows within OVL_ROWS of each neighbour
+  // (their cone reaches the interior rows of launch m-1: wait for it). st: the
+  // interior rows (they never read halo rows; wait for launch m-1's boundary
+  // rows), concurrently.
   template <int CASE>
-  void pair_overlapped(int m, int k, int bin, int bout) {
+  void multi_overlapped(int m, int k, int n, int ka, int kb, int bin, int bout) {
     const Strip& s = S[0];
     double* pin = s.b[bin];
     double* pout = s.b[bout];
@@ -497,7 +531,7 @@ class Solver {
     exchange(bin, HALO, st_b);
     if (m > 0) {
       HIPC(hipStreamWaitEvent(st_b, ev_int[pe], 0));
-      allreduce_pair_slots(k - 2, st_b);  // pair m-1, tested by launch m+1
+      flush_allreduce(st_b);  // launch m-1's residuals, tested by launch m+1
     }
     PairPlan pb{};
     pb.ctiles = (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC;
@@ -506,48 +540,46 @@ class Solver {
     pb.lo1 = g.wj1 + 1 - hi_b; pb.hi1 = g.wj1 + 1;
     pb.nb0 = pb.nbe0 = lo_b ? 1 : 0;
     pb.nb1 = pb.nbe1 = hi_b ? 1 : 0;
-    launch_pair<CASE>(pb, g, pin, pout, s.b[B_F], ctl, k, st_b, 1);
+    launch_multi<CASE>(n, pb, g, pin, pout, s.b[B_F], ctl, k, ka, kb, st_b);
     if (m > 0) HIPC(hipStreamWaitEvent(st, ev_bnd[pe], 0));
-    const PairPlan pi = pair_plan(g.wj0 + lo_b, g.wj1 + 1 - hi_b, 0, 0, resident_pair_waves - 2 * pb.ctiles);
-    launch_pair<CASE>(pi, g, pin, pout, s.b[B_F], ctl, k, st, 1);
-    check_launch("poisson pair (overlapped)");
+    const PairPlan pi =
+        multi_plan(g.wj0 + lo_b, g.wj1 + 1 - hi_b, 0, 0, resident_pair_waves - 2 * pb.ctiles, n);
+    launch_multi<CASE>(n, pi, g, pin, pout, s.b[B_F], ctl, k, ka, kb, st);
+    check_launch("poisson (overlapped)");
     HIPC(hipEventRecord(ev_int[e], st));
     HIPC(hipEventRecord(ev_bnd[e], st_b));
+    ar_pending = {k, n};
     last_bnd = e;
     b_pending = true;
     ++n_overlapped;
   }
 
-  void poisson_launch(int m, int k, int sweeps, int base, bool replay = false, bool after_pair = false) {
+  // SOR launch number m (0-based) of a solve starting in buffer `base`: reads
+  // buffer (base+m) mod nbufs, writes the next. Iterations k .. k+n-1; tests
+  // iterations [ka, kb] first. replay: recomputes iterations of a launch that
+  // already ran (no test, no all-reduce).
+  void poisson_launch(int m, int k, int n, int base, int ka, int kb, bool replay) {
     const int bin = pbuf((base + m) % nbufs());
     const int bout = pbuf((base + m + 1) % nbufs());
-    if (overlap && sweeps == 2 && !replay && kernel_variant == 0) {
-      if (P.case_id == CFD_CAVITY) pair_overlapped<CAVITY>(m, k, bin, bout);
-      else if (P.case_id == CFD_CHANNEL) pair_overlapped<CHANNEL>(m, k, bin, bout);
-      else pair_overlapped<BACKSTEP>(m, k, bin, bout);
+    if (overlap && n >= 2 && !replay && kernel_variant == 0) {
+      if (P.case_id == CFD_CAVITY) multi_overlapped<CAVITY>(m, k, n, ka, kb, bin, bout);
+      else if (P.case_id == CFD_CHANNEL) multi_overlapped<CHANNEL>(m, k, n, ka, kb, bin, bout);
+      else multi_overlapped<BACKSTEP>(m, k, n, ka, kb, bin, bout);
       return;
     }
     join_b();
-    const bool notest = lagged() && !replay;  // lagged mode: a single launch tests nothing (the host does)
-    if (multi()) exchange(bin, sweeps == 2 ? HALO : 4);
+    flush_allreduce(st);  // an overlapped launch before this one
+    if (multi()) exchange(bin, n >= 2 ? HALO : 4);
     std::vector<const double*> pin(S.size());
     std::vector<double*> pout(S.size());
     for (size_t q = 0; q < S.size(); ++q) {
       pin[q] = S[q].b[bin];
       pout[q] = S[q].b[bout];
     }
-    const bool skip = replay || notest;  // launch without the convergence test
-    if (P.case_id == CFD_CAVITY) launch_poisson<CAVITY>(pin.data(), pout.data(), k, sweeps, skip, after_pair);
-    else if (P.case_id == CFD_CHANNEL) launch_poisson<CHANNEL>(pin.data(), pout.data(), k, sweeps, skip, after_pair);
-    else launch_poisson<BACKSTEP>(pin.data(), pout.data(), k, sweeps, skip, after_pair);
-    if (comm && comm->nranks > 1 && !replay) {
-      for (int kk = k; kk < k + sweeps; ++kk) {
-        if (kk % P.check_every == 0 || kk == P.max_iters) {
-          double* slot = ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-          comm_allreduce_max(comm, slot, RES_SHARDS * SHARD_STRIDE, st);
-        }
-      }
-    }
+    if (P.case_id == CFD_CAVITY) launch_poisson<CAVITY>(pin.data(), pout.data(), k, n, ka, kb, replay);
+    else if (P.case_id == CFD_CHANNEL) launch_poisson<CHANNEL>(pin.data(), pout.data(), k, n, ka, kb, replay);
+    else launch_poisson<BACKSTEP>(pin.data(), pout.data(), k, n, ka, kb, replay);
+    if (comm && comm->nranks > 1 && !replay) allreduce_slots(k, n, st);
   }
 
   // solverPressurePoisson (cavity-01.cpp:609-690, channel-01.cpp:635-688,
@@ -609,21 +641,33 @@ class Solver {
     }
     solve_tolerance();
     if (multi()) exchange(B_F, HALO - 1);
-    // Launch plan: pairs of iterations (k, k+1) per launch, a single launch for
-    // an odd last iteration; launch m reads buffer (base+m)&1.
-    const int spl = (P.sweeps_per_launch == 1 || kernel_variant != 0) ? 1 : 2;  // pairs: wave kernels only
+    // Launch plan: spl iterations per launch (3 for the cavity, 2 otherwise,
+    // 1 with sweeps_per_launch = 1 or a legacy kernel), a shorter last launch
+    // for the remainder. Launch m reads buffer (base+m) mod nbufs and tests the
+    // iterations of launch m-1 (lagged: m-2); iteration 0 = initial residual.
+    const int spl = sweeps_per_launch();
     const int chunk = P.chunk > 0 ? P.chunk : 32;  // launches between host polls
+    const int lag = lagged() ? 1 : 0;
+    launches.clear();
+    ar_pending = {0, 0};
     HIPC(hipEventRecord(ev_a, st));
     int k = 0, c = 0, m = 0;
-    int last_tested = -1;  // highest iteration whose residual a launch tests (0: the initial one)
-    const int lag = lagged() ? 1 : 0;
+    int last_tested = -1;  // highest iteration some launch tests
     bool stopped = false;
     while (k < P.max_iters && !stopped) {
       for (int j = 0; j < chunk && k < P.max_iters; ++j, ++m) {
         const int n = std::min(spl, P.max_iters - k);
-        poisson_launch(m, k + 1, n, base, false, spl == 2 && k > 0);
-        if (n == 2) last_tested = std::max(last_tested, k - 2 * lag);
-        else if (!lag) last_tested = std::max(last_tested, k);
+        const int src = m - 1 - lag;
+        int ka = 1, kb = 0;  // empty window
+        if (src >= 0) {
+          ka = launches[src].first;
+          kb = ka + launches[src].n - 1;
+        } else if (src == -1) {
+          ka = kb = 0;
+        }
+        poisson_launch(m, k + 1, n, base, ka, kb, false);
+        if (ka <= kb) last_tested = std::max(last_tested, kb);
+        launches.push_back({k + 1, n});
         k += n;
       }
       join_b();
@@ -635,10 +679,7 @@ class Solver {
       }
       ++c;
     }
-    if (lagged() && k >= 2) {  // the last pair's all-reduce (no later launch enqueued it)
-      const int klast = (P.max_iters & 1) && k == P.max_iters ? k - 2 : k - 1;
-      allreduce_pair_slots(klast, st);
-    }
+    flush_allreduce(st);  // overlapped launches all-reduce one launch late: the last one
     HIPC(hipEventRecord(ev_b, st));
     int iters;
     if (c > 0) {
@@ -651,8 +692,8 @@ class Solver {
     HIPC(hipEventSynchronize(ev_b));
     float ms = 0.f;
     HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
-    // iterations after the last one a launch tested (the last pair(s), and the
-    // initial residual if no launch tested it): test them here, in order (the
+    // iterations after the last one a launch tested (the last launch(es), and
+    // the initial residual if no launch tested it): tested here, in order (the
     // reference's while condition, cavity-01.cpp:633)
     if (iters == P.max_iters && last_tested < P.max_iters - 1) {
       double t2[2];
@@ -675,26 +716,34 @@ class Solver {
         }
       }
     }
-    // an odd last iteration that ran as the first of a pair: its pair wrote
-    // iteration iters+1; recompute iteration iters from the pair's input
-    if (spl == 2 && iters > 0 && (iters & 1) && !(iters == P.max_iters && (P.max_iters & 1))) {
-      HIPC(hipEventRecord(ev_a, st));
-      poisson_launch((iters - 1) / 2, iters, 1, base, true);
-      HIPC(hipEventRecord(ev_b, st));
-      HIPC(hipEventSynchronize(ev_b));
-      float ms2 = 0.f;
-      HIPC(hipEventElapsedTime(&ms2, ev_a, ev_b));
-      ms += ms2;
+    // the launch that computed iteration `iters`; if it ran further, redo the
+    // first r of its iterations from its (intact) input into its output buffer
+    int last = -1, replayed = 0;
+    long long work_sweeps = 0;
+    if (iters > 0) {
+      for (size_t q = 0; q < launches.size(); ++q) {
+        work_sweeps += launches[q].n;
+        if (iters <= launches[q].first + launches[q].n - 1) {
+          last = (int)q;
+          break;
+        }
+      }
+      const int r = iters - launches[last].first + 1;
+      if (r < launches[last].n) {
+        HIPC(hipEventRecord(ev_a, st));
+        poisson_launch(last, launches[last].first, r, base, 1, 0, true);
+        HIPC(hipEventRecord(ev_b, st));
+        HIPC(hipEventSynchronize(ev_b));
+        float ms2 = 0.f;
+        HIPC(hipEventElapsedTime(&ms2, ev_a, ev_b));
+        ms += ms2;
+        replayed = r;
+      }
     }
     // launches that did work (later ones in the enqueued chunks exit at entry)
-    long long work_launches = (iters + spl - 1) / spl, work_sweeps = iters;
-    if (spl == 2 && (iters & 1) && !(iters == P.max_iters && (P.max_iters & 1))) {
-      work_launches += 1;  // the replay
-      work_sweeps += 2;    // the pair computed iteration iters+1, the replay redid iters
-    }
     T.poisson_ms += ms;
-    T.poisson_launches += work_launches;
-    T.poisson_sweeps += work_sweeps;
+    T.poisson_launches += (last + 1) + (replayed ? 1 : 0);
+    T.poisson_sweeps += work_sweeps + replayed;
     T.poisson_overlapped += n_overlapped;
     n_overlapped = 0;
     long long owned = 0;
@@ -711,10 +760,8 @@ class Solver {
       res = 0.0;
       for (int q = 0; q < RES_SHARDS; ++q) res = std::max(res, h_shard[q * SHARD_STRIDE]);
     }
-    // launch m's output is buffer (base+m+1) mod nbufs; iteration `iters` was
-    // written by launch ceil(iters/spl)-1 (or its replay, into the same buffer)
-    const int last_launch = (iters + spl - 1) / spl;
-    pcur = (base + last_launch) % nbufs();
+    // launch m's output is buffer (base+m+1) mod nbufs (the replay writes there too)
+    pcur = (base + last + 1) % nbufs();
     if (out) {
       out->sor_iterations = iters;
       out->residual = res;

@@ -1,13 +1,13 @@
-"""Two SOR iterations per launch (poisson_pair_kernel) against one per launch
-(poisson_wave_kernel): the fused launch must be invisible — same iteration
-counts, same residuals, same fields, bit for bit — including the edge cases
-of the launch plan (csrc/solver.hip, Solver::solve):
+"""Several SOR iterations per launch (poisson_multi_kernel: 2, or 3 for the
+cavity) against one per launch (poisson_wave_kernel): the fused launch must be
+invisible — same iteration counts, same residuals, same fields, bit for bit —
+including the edge cases of the launch plan (csrc/solver.hip, Solver::solve):
 
-* a solve that stops at an odd iteration count (the pair already computed
-  one more iteration; the host replays the odd one from the pair's input);
-* an iteration cap that is odd (last launch is a single iteration) or even
-  with convergence exactly at cap-1 (tested on the host after the loop);
-* row strips (8-row halos exchanged once per pair) and check_every > 1.
+* a solve that stops inside a launch (the launch already computed further;
+  the host replays the first r of its iterations from the launch's input);
+* an iteration cap that leaves a shorter last launch, or whose last
+  iterations no launch tested (tested on the host after the loop);
+* row strips (8-row halos exchanged once per launch) and check_every > 1.
 """
 from __future__ import annotations
 
@@ -33,12 +33,13 @@ def run(case, cp, steps, **kw):
     return hist, out, tm
 
 
-@pytest.mark.parametrize("case", ["cavity", "channel", "backwards_step"])
-def test_pairs_equal_single_sweeps(case):
+@pytest.mark.parametrize("case,spl", [("cavity", 2), ("cavity", 3), ("cavity", 0), ("channel", 2), ("channel", 0),
+                                      ("backwards_step", 2)])
+def test_pairs_equal_single_sweeps(case, spl):
     cp = C.reference_defaults(case)
     steps = 6 if case != "backwards_step" else 2
     h1, f1, t1 = run(case, cp, steps, sweeps_per_launch=1)
-    h2, f2, t2 = run(case, cp, steps, sweeps_per_launch=2)
+    h2, f2, t2 = run(case, cp, steps, sweeps_per_launch=spl)
     assert h1 == h2
     for n in FIELDS:
         assert_bits(f2[n], f1[n], f"{case} {n}")
@@ -46,32 +47,35 @@ def test_pairs_equal_single_sweeps(case):
     assert t1.poisson_sweeps == t1.poisson_launches
 
 
-def test_odd_stop_is_replayed_and_matches_oracle():
+@pytest.mark.parametrize("spl", [2, 3])
+def test_stop_inside_a_launch_is_replayed_and_matches_oracle(spl):
     cp = C.reference_defaults("cavity")
-    g = C.CavitySolver(cp, device=0, sweeps_per_launch=2)
+    g = C.CavitySolver(cp, device=0, sweeps_per_launch=spl)
     o = O.Oracle(cp, ordering=O.RB)
     it_g, res_g = g.step()
     it_o, res_o = o.step()
     assert (it_g, res_g) == (it_o, res_o)
-    assert it_g % 2 == 1, "fixture meant to stop at an odd count (replay path)"
+    r = it_g % spl  # iterations of the stopping launch that count
+    assert r != 0, "fixture meant to stop inside a launch (replay path)"
     tm = g.timing()
-    assert tm.poisson_launches == (it_g + 1) // 2 + 1  # (it+1)/2 pairs, then one replayed iteration
-    assert tm.poisson_sweeps == it_g + 2
-    assert_bits(g.field("p"), o.field("p"), "p after an odd stop")
+    full = (it_g - r) // spl + 1  # launches up to the stopping one
+    assert tm.poisson_launches == full + 1  # ... then one replay launch
+    assert tm.poisson_sweeps == full * spl + r
+    assert_bits(g.field("p"), o.field("p"), "p after a stop inside a launch")
     g.close()
 
 
-@pytest.mark.parametrize("delta", [-1, 0, 1, 2])
-def test_iteration_cap_edges(delta):
-    """cap = K + delta around the natural stop K (odd): cap K-1 (even, not
-    converged), K (odd cap, single last launch), K+1 (even cap, convergence at
-    cap-1 found by the host check), K+2 (converges inside the pairs)."""
+@pytest.mark.parametrize("spl", [2, 3])
+@pytest.mark.parametrize("delta", [-2, -1, 0, 1, 2, 3])
+def test_iteration_cap_edges(spl, delta):
+    """cap = K + delta around the natural stop K: caps below K (not converged,
+    shorter last launches), at K, and above K (the stop found by a launch, or
+    by the host's test of the iterations no launch tested)."""
     base = C.reference_defaults("cavity")
     K, _ = C.CavitySolver(base, device=0, sweeps_per_launch=1).step()
-    assert K % 2 == 1
     cp = C.make_params("cavity", max_iters=K + delta)
     h1, f1, _ = run("cavity", cp, 1, sweeps_per_launch=1)
-    h2, f2, _ = run("cavity", cp, 1, sweeps_per_launch=2)
+    h2, f2, _ = run("cavity", cp, 1, sweeps_per_launch=spl)
     assert h1 == h2
     assert h1[0][0] == min(K, K + delta)
     assert_bits(f2["p"], f1["p"], f"p cap K{delta:+d}")
@@ -82,7 +86,7 @@ def test_iteration_cap_edges(delta):
 def test_pairs_on_strips(case, check_every):
     cp = C.reference_defaults(case)
     h1, f1, _ = run(case, cp, 3, sweeps_per_launch=1, check_every=check_every)
-    h2, f2, _ = run(case, cp, 3, sweeps_per_launch=2, check_every=check_every, n_strips=3)
+    h2, f2, _ = run(case, cp, 3, sweeps_per_launch=0, check_every=check_every, n_strips=3)
     assert [k for k, _ in h1] == [k for k, _ in h2]
     tol = 0.0 if case == "cavity" else 1e-12
     for n in FIELDS:
@@ -92,11 +96,12 @@ def test_pairs_on_strips(case, check_every):
             np.testing.assert_allclose(f2[n], f1[n], rtol=0, atol=tol * max(1.0, np.abs(f1[n]).max()))
 
 
-def test_pairs_full_size_bitexact():
-    """BASELINE configs[1] size (4096^2): 31 sweeps (15 pairs + 1 single) == 31
-    single launches, bit for bit."""
+@pytest.mark.parametrize("spl", [2, 3])
+def test_pairs_full_size_bitexact(spl):
+    """BASELINE configs[1] size (4096^2): 31 sweeps (15 pairs + 1 single, or 10
+    triples + 1 single) == 31 single launches, bit for bit."""
     cp = C.make_params("cavity", nx=4096, ny=4096, max_iters=31)
     h1, f1, _ = run("cavity", cp, 1, sweeps_per_launch=1)
-    h2, f2, _ = run("cavity", cp, 1, sweeps_per_launch=2)
+    h2, f2, _ = run("cavity", cp, 1, sweeps_per_launch=spl)
     assert h1 == h2 and h1[0][0] == 31
     assert_bits(f2["p"], f1["p"], "p 4096^2")
