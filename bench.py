@@ -193,7 +193,7 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "poisson_pair_kernel<cavity>" if sweeps_per_launch > 1.5 else "poisson_wave_kernel<cavity>",
+                "kernel": ("poisson_multi_kernel<cavity,3>" if sweeps_per_launch > 2.5 else "poisson_multi_kernel<cavity,2>" if sweeps_per_launch > 1.5 else "poisson_wave_kernel<cavity>"),
                 "bytes_per_launch": BYTES_PER_CELL * cells_per_launch,
                 "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "sweeps_per_launch": round(sweeps_per_launch, 4),

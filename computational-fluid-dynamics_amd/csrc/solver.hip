@@ -135,7 +135,7 @@ class Solver {
   int kernel_variant = 0;  // 0: wave march (default), 1: fused LDS tile, 2: block column march
   int resident_waves = 2048;  // wave-march tiles in flight (CUs x 4 SIMDs x waves per SIMD)
   int resident_pair_waves = 2048;  // the same for the two-iteration kernel
-  int pair_edge_pct = 53;          // boundary-column band length, % of the interior march (swept: 50-56 best)
+  int pair_edge_pct = 45;          // boundary-column band length, % of the interior march (swept, cavity triples: 40-47 best)
   int resident_blocks = 1024;  // march-kernel blocks resident at once on this device
   int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order
   int march_min_th = MARCH_MIN_TH;
