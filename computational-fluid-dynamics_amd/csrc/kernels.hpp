@@ -1331,8 +1331,18 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     double2 nv = m;
     if (CASE != CAVITY && FAST) {  // interior columns: only the ghost rows refresh (row-uniform)
       const int j = A - 3 * DIR;
-      if (j == 0) nv = CFD_N(W[CFD_SLOT(4 + OFF)], W[CFD_SLOT(2 + OFF)]);       // p[0][i] = p[1][i]
-      if (j == ny + 1) nv = CFD_S(W[CFD_SLOT(4 + OFF)], W[CFD_SLOT(2 + OFF)]);  // p[ny+1][i] = p[ny][i]
+      // values picked at compile time: a ?: between the two ring elements
+      // became a select of addresses, which put the whole ring in scratch
+      double2 wn, ws;
+      if constexpr (DIR > 0) {
+        wn = W[CFD_SLOT(2 + OFF)];
+        ws = W[CFD_SLOT(4 + OFF)];
+      } else {
+        wn = W[CFD_SLOT(4 + OFF)];
+        ws = W[CFD_SLOT(2 + OFF)];
+      }
+      if (j == 0) nv = wn;       // p[0][i] = p[1][i]
+      if (j == ny + 1) nv = ws;  // p[ny+1][i] = p[ny][i]
     }
     if (CASE != CAVITY && !FAST) {
       const int j = A - 3 * DIR;
@@ -1772,9 +1782,8 @@ __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAI
     if (fast) {
       if (up) wave_march_pair<CASE, -1, true>(x, y0, y1, r1, r2);
       else wave_march_pair<CASE, 1, true>(x, y0, y1, r1, r2);
-    } else {
-      if (up) wave_march_pair_edge<CASE, -1>(x, y0, y1, r1, r2);
-      else wave_march_pair_edge<CASE, 1>(x, y0, y1, r1, r2);
+    } else {  // boundary-column waves march one way (compact code)
+      wave_march_pair_edge<CASE, 1>(x, y0, y1, r1, r2);
     }
     r[0] = r1;
     r[NS - 1] = r2;
