@@ -10,8 +10,10 @@ All inputs are device-resident when the timed region starts.
   value = interior cells x SOR iterations summed over all ranks / wall time of
           the K timed steps (max over ranks), in MLUPS.
 
-Extra fields: steps_per_sec, roofline (fused red-black SOR kernel, HIP events on
-the solver's stream over the timed region), cpu_baseline (the oracle's
+Extra fields: steps_per_sec, roofline (the fused red-black SOR kernel, three
+sweeps per launch for the cavity: HIP events on the solver's stream over the
+timed region; `achieved` = the 24 B/cell one launch must move / launch time,
+`effective_sweep_*` the same per sweep), cpu_baseline (the oracle's
 lexicographic SOR loop — the reference's loop restated in C — on a bounded
 sample of the same grid, rank 0 only).
 
@@ -77,7 +79,7 @@ def main() -> int:
     ap.add_argument("--max-iters", type=int, default=10000)
     ap.add_argument("--check-every", type=int, default=0, help="residual test cadence (0: 1 on 1 GPU, 8 on >1)")
     ap.add_argument("--sweeps-per-launch", type=int, default=0,
-                    help="red-black SOR iterations fused per kernel launch (0: auto = 2)")
+                    help="red-black SOR iterations fused per kernel launch (0: auto = 3 for the cavity)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

@@ -39,8 +39,9 @@ class _SolverBase:
                  ordering: str = "rb", sweeps_per_launch: int = 0):
         """ordering: "rb" (red-black SOR, the fast default) or "lex" (the reference's
         lexicographic sweep, bit-identical to it; one device, one strip).
-        sweeps_per_launch: red-black iterations fused per kernel launch (0 = auto = 2,
-        1 or 2); the result is bit-identical either way."""
+        sweeps_per_launch: red-black iterations fused per kernel launch (0 = auto: 3
+        for the cavity, 2 otherwise; 1, 2, or 3 for the cavity); bit-identical
+        either way."""
         self.params = params if params is not None else make_params(self.CASE)
         if self.params.case_id != self.CASE:
             raise ValueError(f"{type(self).__name__} needs case {CASE_NAMES[self.CASE]}")

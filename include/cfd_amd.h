@@ -66,8 +66,8 @@ typedef struct cfd_params {
   int chunk;            /* SOR launches enqueued between host polls (0 = auto) */
   int ordering;         /* CFD_ORDER_RB (default, multi-block, strips/ranks) or CFD_ORDER_LEX
                            (the reference's sweep order, bit-identical; one device, one strip) */
-  int sweeps_per_launch; /* red-black SOR iterations fused into one kernel launch: 0 = auto (2),
-                           1 or 2; results are bit-identical either way */
+  int sweeps_per_launch; /* red-black SOR iterations fused into one kernel launch: 0 = auto (3 for
+                           the cavity, 2 otherwise), 1, 2 or 3 (cavity); bit-identical either way */
 } cfd_params;
 
 enum cfd_ordering { CFD_ORDER_RB = 0, CFD_ORDER_LEX = 1 };
@@ -90,7 +90,7 @@ typedef struct cfd_timing {
   long long poisson_cell_updates; /* interior cells x active iterations (this rank) */
   double step_ms;             /* device time of whole timesteps */
   long long steps;
-  long long poisson_sweeps;   /* SOR iterations executed by those launches (2 per fused launch) */
+  long long poisson_sweeps;   /* SOR iterations executed by those launches (up to 3 per fused launch) */
   long long poisson_overlapped; /* pair launches split into interior + halo-overlapped boundary rows (ranks) */
 } cfd_timing;
 
