@@ -4,9 +4,9 @@ The GPU data path (RCCL send/recv of halo rows inside libcfd_amd.so) needs
 GPUs; here we check the host logic around it and the decomposition itself:
 row partitioning, RCCL-id bootstrap over a process group, max-over-ranks
 timing, and a numpy emulation of the fused red-black SOR launches on two
-strips: HALO=8 rows exchanged over gloo, then two iterations computed locally
-(the GPU's two-iteration kernel, poisson_pair_kernel), a single one for an odd
-last iteration. It must equal the single-domain iteration bit for bit, both
+strips: HALO=8 rows exchanged over gloo, then two or three iterations computed locally
+(the GPU's multi-iteration kernel, poisson_multi_kernel: 2, or 3 for the
+cavity), a shorter last launch for the remainder. It must equal the single-domain iteration bit for bit, both
 residuals included (the property the GPU kernels rely on: redundant
 recomputation of the halo rows reproduces the neighbour's arithmetic).
 """
@@ -72,7 +72,7 @@ def residual(p, f, nx, ny, h, j_lo):
     return np.where(inside, np.abs(r), 0.0)
 
 
-def _worker(rank, world, port, q, nx, ny, iters):
+def _worker(rank, world, port, q, nx, ny, iters, spl):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import torch
@@ -96,7 +96,7 @@ def _worker(rank, world, port, q, nx, ny, iters):
         res_hist = []
         done = 0
         while done < iters:
-            n = min(2, iters - done)  # iterations fused into this launch
+            n = min(spl, iters - done)  # iterations fused into this launch
             # exchange HALO owned rows with the neighbours (the GPU path: ncclSend/ncclRecv)
             if rank > 0:
                 dist.send(torch.from_numpy(p[HALO:2 * HALO].copy()), rank - 1)
@@ -124,13 +124,14 @@ def _worker(rank, world, port, q, nx, ny, iters):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("spl", [2, 3])
 @pytest.mark.parametrize("world", [2])
-def test_two_rank_strips_equal_single_domain(world):
+def test_two_rank_strips_equal_single_domain(world, spl):
     nx, ny, iters = 24, 20, 15
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, nx, ny, iters)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, nx, ny, iters, spl)) for r in range(world)]
     for pr in procs:
         pr.start()
     out = [q.get(timeout=120) for _ in range(world)]

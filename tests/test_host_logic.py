@@ -81,6 +81,16 @@ def test_invalid_params_rejected():
     assert b"unknown case" in _lib.lib().cfd_last_error()
 
 
+@pytest.mark.parametrize("case,spl,msg", [("channel", 3, b"cavity only"), ("cavity", 4, b"sweeps_per_launch"),
+                                          ("cavity", -1, b"sweeps_per_launch")])
+def test_sweeps_per_launch_validated_before_device(case, spl, msg):
+    """Parameter errors are reported before any device is touched (the checks
+    run first in the solver constructor), so they hold on CPU-only hosts too."""
+    with pytest.raises(_lib.CfdError) as e:
+        C.solver_for(C.make_params(case), sweeps_per_launch=spl)
+    assert msg.decode() in str(e.value)
+
+
 def test_no_cpu_fallback_without_gpu():
     """cfd_create must fail loudly when there is no gfx950 device (here: no GPU at all)."""
     probe = subprocess.run(["python", "-c", "import torch;print(torch.cuda.is_available())"], capture_output=True,
