@@ -35,20 +35,21 @@ sys.path.insert(0, os.path.join(ROOT, "computational-fluid-dynamics_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_CELL = 24.0  # SOR launch: read p_in + read f + write p_out, fp64
 METRIC = "Poisson MLUPS + steps/sec, cavity 4096² @1/2/4/8 GPU; % HBM roofline"
+WORKLOAD = {"cavity": "lid-driven cavity", "channel": "channel flow", "backwards_step": "backwards-facing step"}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(nx: int, ny: int, budget_s: float) -> dict:
+def cpu_baseline(nx: int, ny: int, budget_s: float, case: str = "cavity") -> dict:
     """The reference's SOR loop (sweep + residual per iteration, cavity-01.cpp:635-678)
     restated in C (oracle/), single core, on the same grid for a bounded time."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from cfd_amd.params import make_params
 
-    cp = make_params("cavity", nx=nx, ny=ny)
+    cp = make_params(case, nx=nx, ny=ny)
     o = O.Oracle(cp, ordering=O.LEX)
     o.velocity_bc(False)
     o.tentative()
@@ -65,7 +66,7 @@ def cpu_baseline(nx: int, ny: int, budget_s: float) -> dict:
     mlups = nx * ny * n / el / 1e6
     return {"value": round(mlups, 3), "unit": "MLUPS", "cores": 1, "kind": "port",
             "sample": f"{n} lexicographic SOR sweeps + residual (reference loop restated in C, gcc -O2) on the "
-                      f"{nx}x{ny} cavity after one predictor step, {el:.1f} s single-threaded"}
+                      f"{nx}x{ny} {case} after one predictor step, {el:.1f} s single-threaded"}
 
 
 def main() -> int:
@@ -76,6 +77,8 @@ def main() -> int:
     ap.add_argument("--nx", type=int, default=4096)
     ap.add_argument("--ny", type=int, default=4096, help="rows per GPU (weak scaling)")
     ap.add_argument("--re", type=float, default=1000.0)
+    ap.add_argument("--case", default="cavity", choices=["cavity", "channel", "backwards_step"],
+                    help="workload (the metric is quoted on the cavity; the others are extra measurements)")
     ap.add_argument("--max-iters", type=int, default=10000)
     ap.add_argument("--check-every", type=int, default=0, help="residual test cadence (0: 1 on 1 GPU, 8 on >1)")
     ap.add_argument("--sweeps-per-launch", type=int, default=0,
@@ -102,23 +105,24 @@ def main() -> int:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     check_every = args.check_every or (1 if world == 1 else 8)
-    cp = C.make_params("cavity", re=args.re, nx=args.nx, ny=args.ny * world, max_iters=args.max_iters)
+    cp = C.make_params(args.case, re=args.re, nx=args.nx, ny=args.ny * world, max_iters=args.max_iters)
     comm = None
     if world > 1:
         from cfd_amd.dist import init_comm, weak_rows
         comm = init_comm(dist, rank, world, local_rank)
         rows = weak_rows(rank, args.ny)
-        solver = C.CavitySolver(cp, device=local_rank, check_every=check_every, rank_rows=rows, comm=comm,
-                                sweeps_per_launch=args.sweeps_per_launch)
+        solver = C.solver_for(cp, device=local_rank, check_every=check_every, rank_rows=rows, comm=comm,
+                              sweeps_per_launch=args.sweeps_per_launch)
     else:
-        solver = C.CavitySolver(cp, device=local_rank, check_every=check_every,
-                                sweeps_per_launch=args.sweeps_per_launch)
+        solver = C.solver_for(cp, device=local_rank, check_every=check_every,
+                              sweeps_per_launch=args.sweeps_per_launch)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    solver.applyBoundaryConditions()
+    if args.case == "cavity":  # cavity-01.cpp:380 (the open cases apply their BCs in the constructor)
+        solver.applyBoundaryConditions()
     for _ in range(args.warmup):
         solver.step()
     solver.synchronize()
@@ -180,7 +184,7 @@ def main() -> int:
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"lid-driven cavity Re={args.re:g}, {cp.nx}x{args.ny} fp64 cells per GPU "
+                "workload": f"{WORKLOAD[args.case]} Re={args.re:g}, {cp.nx}x{args.ny} fp64 cells per GPU "
                             f"(global {cp.nx}x{cp.ny}), reference SOR tolerance {cp.tol_factor:g}*max|src|, "
                             f"cap {cp.max_iters} sweeps/step",
                 "nx": cp.nx, "ny_per_gpu": args.ny, "global_ny": cp.ny,
@@ -195,7 +199,9 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": ("poisson_multi_kernel<cavity,3>" if sweeps_per_launch > 2.5 else "poisson_multi_kernel<cavity,2>" if sweeps_per_launch > 1.5 else "poisson_wave_kernel<cavity>"),
+                "kernel": (f"poisson_multi_kernel<{args.case},3>" if sweeps_per_launch > 2.5
+                           else f"poisson_multi_kernel<{args.case},2>" if sweeps_per_launch > 1.5
+                           else f"poisson_wave_kernel<{args.case}>"),
                 "bytes_per_launch": BYTES_PER_CELL * cells_per_launch,
                 "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "sweeps_per_launch": round(sweeps_per_launch, 4),
@@ -205,7 +211,7 @@ def main() -> int:
         }
         if not args.no_cpu_baseline:
             log("timing the CPU baseline ...")
-            line["cpu_baseline"] = cpu_baseline(cp.nx, args.ny, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(cp.nx, args.ny, args.cpu_seconds, args.case)
         print(json.dumps(line), flush=True)
 
     solver.close()
