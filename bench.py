@@ -35,7 +35,8 @@ sys.path.insert(0, os.path.join(ROOT, "computational-fluid-dynamics_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_CELL = 24.0  # SOR launch: read p_in + read f + write p_out, fp64
 METRIC = "Poisson MLUPS + steps/sec, cavity 4096² @1/2/4/8 GPU; % HBM roofline"
-WORKLOAD = {"cavity": "lid-driven cavity", "channel": "channel flow", "backwards_step": "backwards-facing step"}
+WORKLOAD = {"cavity": "lid-driven cavity", "channel": "channel flow", "backwards_step": "backwards-facing step",
+            "rayleigh_benard": "Rayleigh-Benard convection"}
 
 
 def log(*a):
@@ -77,8 +78,9 @@ def main() -> int:
     ap.add_argument("--nx", type=int, default=4096)
     ap.add_argument("--ny", type=int, default=4096, help="rows per GPU (weak scaling)")
     ap.add_argument("--re", type=float, default=1000.0)
-    ap.add_argument("--case", default="cavity", choices=["cavity", "channel", "backwards_step"],
+    ap.add_argument("--case", default="cavity", choices=["cavity", "channel", "backwards_step", "rayleigh_benard"],
                     help="workload (the metric is quoted on the cavity; the others are extra measurements)")
+    ap.add_argument("--ra", type=float, default=1e6, help="Rayleigh number (--case rayleigh_benard)")
     ap.add_argument("--max-iters", type=int, default=10000)
     ap.add_argument("--check-every", type=int, default=0, help="residual test cadence (0: 1 on 1 GPU, 8 on >1)")
     ap.add_argument("--sweeps-per-launch", type=int, default=0,
@@ -105,7 +107,10 @@ def main() -> int:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     check_every = args.check_every or (1 if world == 1 else 8)
-    cp = C.make_params(args.case, re=args.re, nx=args.nx, ny=args.ny * world, max_iters=args.max_iters)
+    if args.case == "rayleigh_benard":  # BASELINE configs[4]: Pr 0.71, the Ra given
+        cp = C.make_params(args.case, ra=args.ra, nx=args.nx, ny=args.ny * world, max_iters=args.max_iters)
+    else:
+        cp = C.make_params(args.case, re=args.re, nx=args.nx, ny=args.ny * world, max_iters=args.max_iters)
     comm = None
     if world > 1:
         from cfd_amd.dist import init_comm, weak_rows
@@ -170,6 +175,7 @@ def main() -> int:
             except Exception:
                 traffic = None
         mlups = updates / elapsed / 1e6
+        kcase = "cavity" if args.case == "rayleigh_benard" else args.case  # RB runs the cavity SOR kernel
         line = {
             "metric": METRIC,
             "value": round(mlups, 2),
@@ -184,7 +190,9 @@ def main() -> int:
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"{WORKLOAD[args.case]} Re={args.re:g}, {cp.nx}x{args.ny} fp64 cells per GPU "
+                "workload": f"{WORKLOAD[args.case]} "
+                            + (f"Ra={cp.ra:g} Pr={cp.pr:g}" if args.case == "rayleigh_benard" else f"Re={args.re:g}")
+                            + f", {cp.nx}x{args.ny} fp64 cells per GPU "
                             f"(global {cp.nx}x{cp.ny}), reference SOR tolerance {cp.tol_factor:g}*max|src|, "
                             f"cap {cp.max_iters} sweeps/step",
                 "nx": cp.nx, "ny_per_gpu": args.ny, "global_ny": cp.ny,
@@ -199,9 +207,9 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": (f"poisson_multi_kernel<{args.case},3>" if sweeps_per_launch > 2.5
-                           else f"poisson_multi_kernel<{args.case},2>" if sweeps_per_launch > 1.5
-                           else f"poisson_wave_kernel<{args.case}>"),
+                "kernel": (f"poisson_multi_kernel<{kcase},3>" if sweeps_per_launch > 2.5
+                           else f"poisson_multi_kernel<{kcase},2>" if sweeps_per_launch > 1.5
+                           else f"poisson_wave_kernel<{kcase}>"),
                 "bytes_per_launch": BYTES_PER_CELL * cells_per_launch,
                 "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "sweeps_per_launch": round(sweeps_per_launch, 4),

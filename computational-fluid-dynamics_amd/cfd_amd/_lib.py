@@ -18,7 +18,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # kernel build variants, scripts/); the product default is libcfd_amd.so
 LIB_PATH = os.path.join(PKG_DIR, os.environ.get("CFD_AMD_LIB", "libcfd_amd.so"))
 
-CFD_FIELD = {"p": 0, "src": 1, "us": 3, "vs": 4, "u": 5, "v": 6, "uc": 7, "vc": 8}
+CFD_FIELD = {"p": 0, "src": 1, "us": 3, "vs": 4, "u": 5, "v": 6, "uc": 7, "vc": 8, "t": 9}
 COMM_ID_BYTES = 128
 
 
@@ -37,6 +37,9 @@ class CfdParams(ctypes.Structure):
         ("step_i", ctypes.c_int), ("inlet_jmax", ctypes.c_int),
         ("check_every", ctypes.c_int), ("chunk", ctypes.c_int), ("ordering", ctypes.c_int),
         ("sweeps_per_launch", ctypes.c_int),
+        ("ra", ctypes.c_double), ("pr", ctypes.c_double), ("kappa", ctypes.c_double), ("buoyancy", ctypes.c_double),
+        ("t_hot", ctypes.c_double), ("t_cold", ctypes.c_double), ("t_ref", ctypes.c_double),
+        ("t_perturb", ctypes.c_double),
     ]
 
 
@@ -72,6 +75,8 @@ SIGNATURES = {
     "cfd_apply_bc": (_i, [_vp]),
     "cfd_apply_tentative_bc": (_i, [_vp]),
     "cfd_compute_tentative": (_i, [_vp]),
+    "cfd_advance_temperature": (_i, [_vp]),
+    "cfd_params_init_rb": (_i, [_d, _d, _i, _i, _d, ctypes.POINTER(CfdParams)]),
     "cfd_build_source": (_i, [_vp]),
     "cfd_solve_pressure": (_i, [_vp, ctypes.POINTER(StepInfo)]),
     "cfd_apply_correction": (_i, [_vp]),

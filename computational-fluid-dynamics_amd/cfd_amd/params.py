@@ -15,8 +15,8 @@ from __future__ import annotations
 import dataclasses
 import math
 
-CAVITY, CHANNEL, BACKSTEP = 0, 1, 2
-CASE_NAMES = {CAVITY: "cavity", CHANNEL: "channel", BACKSTEP: "backwards_step"}
+CAVITY, CHANNEL, BACKSTEP, RAYLEIGH_BENARD = 0, 1, 2, 3
+CASE_NAMES = {CAVITY: "cavity", CHANNEL: "channel", BACKSTEP: "backwards_step", RAYLEIGH_BENARD: "rayleigh_benard"}
 CASE_IDS = {v: k for k, v in CASE_NAMES.items()}
 
 
@@ -43,10 +43,30 @@ class CaseParams:
     # overrides (0 = derive as the reference does)
     dt_override: float = 0.0
     omega_override: float = 0.0
+    # Rayleigh-Benard (case 3, no reference solver; free-fall units, H = 1)
+    ra: float = 0.0
+    pr: float = 0.0
+    t_hot: float = 1.0
+    t_cold: float = 0.0
+    t_perturb: float = 0.01
+
+    @property
+    def kappa(self) -> float:
+        return 1.0 / math.sqrt(self.ra * self.pr) if self.case_id == RAYLEIGH_BENARD else 0.0
+
+    @property
+    def buoyancy(self) -> float:
+        return 1.0 if self.case_id == RAYLEIGH_BENARD else 0.0
+
+    @property
+    def t_ref(self) -> float:
+        return 0.5 * (self.t_hot + self.t_cold) if self.case_id == RAYLEIGH_BENARD else 0.0
 
     # ---- derived, as in the reference constructors ----
     @property
     def nu(self) -> float:
+        if self.case_id == RAYLEIGH_BENARD:
+            return math.sqrt(self.pr / self.ra)
         if self.case_id == CAVITY:
             return self.rho * self.u_ref * self.length / self.re  # cavity-01.cpp:356
         if self.case_id == CHANNEL:
@@ -59,7 +79,7 @@ class CaseParams:
 
     @property
     def dy(self) -> float:
-        if self.case_id == CAVITY:
+        if self.case_id in (CAVITY, RAYLEIGH_BENARD):
             return self.length / self.nx  # uniform spacing (cavity-01.cpp:357)
         return self.height / self.ny
 
@@ -74,6 +94,9 @@ class CaseParams:
         if self.dt_override > 0:
             return self.dt_override
         nu = self.nu
+        if self.case_id == RAYLEIGH_BENARD:  # diffusive and free-fall (U = 1) limits
+            h = self.dx
+            return self.cfl * min(0.25 * h * h / max(nu, self.kappa), h / 1.0)
         if self.case_id == CAVITY:
             h = self.dx  # cavity-01.cpp:359-360
             return self.cfl * min(0.25 * h * h / nu, h / self.u_ref)
@@ -111,12 +134,15 @@ def reference_defaults(case: int | str) -> CaseParams:
     if case == BACKSTEP:  # backwards_step-01.cpp:319-334
         return CaseParams(BACKSTEP, 256, 32, 8.0, 2.0, 100.0, 1.0, 1.0, 0.2, 15.0, 1e-7, 1e-10, 10000, 10, 10,
                           h_inlet=1.0, step_x=2.0)
+    if case == RAYLEIGH_BENARD:  # BASELINE configs[4]: Ra 1e6, Pr 0.71, aspect 4 (not in the reference tree)
+        return CaseParams(RAYLEIGH_BENARD, 256, 64, 4.0, 1.0, math.sqrt(1e6 / 0.71), 0.0, 1.0, 0.5, 100.0, 1e-9,
+                          0.0, 10000, 100, 100, ra=1e6, pr=0.71)
     raise ValueError(f"unknown case {case}")
 
 
 def make_params(case: int | str, *, re: float | None = None, nx: int | None = None, ny: int | None = None,
                 dt: float | None = None, final_time: float | None = None, max_iters: int | None = None,
-                omega: float | None = None) -> CaseParams:
+                omega: float | None = None, ra: float | None = None, pr: float | None = None) -> CaseParams:
     """Reference defaults with the CLI's overrides applied.
 
     Grid overrides keep the physical domain of the case and change the spacing,
@@ -134,6 +160,12 @@ def make_params(case: int | str, *, re: float | None = None, nx: int | None = No
         p.ny = int(nx)
     if p.case_id == CAVITY:
         p.height = p.ny * p.length / p.nx
+    if p.case_id == RAYLEIGH_BENARD:  # H = 1, dx = dy
+        p.ra = float(ra if ra is not None else (re if re is not None else p.ra))
+        if pr is not None:
+            p.pr = float(pr)
+        p.re = math.sqrt(p.ra / p.pr)
+        p.length = p.nx * p.height / p.ny
     if dt is not None:
         p.dt_override = float(dt)
     if final_time is not None:

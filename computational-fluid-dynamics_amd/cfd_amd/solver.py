@@ -16,7 +16,7 @@ import numpy as np
 
 from . import _lib
 from .logfmt import step_line, warning_line
-from .params import BACKSTEP, CASE_NAMES, CAVITY, CHANNEL, CaseParams, make_params
+from .params import BACKSTEP, CASE_NAMES, CAVITY, CHANNEL, RAYLEIGH_BENARD, CaseParams, make_params
 
 
 def to_cparams(cp: CaseParams, check_every: int = 1, chunk: int = 0, ordering: str = "rb",
@@ -26,7 +26,8 @@ def to_cparams(cp: CaseParams, check_every: int = 1, chunk: int = 0, ordering: s
         cp.case_id, cp.nx, cp.ny, cp.length, cp.height, cp.re, cp.u_ref, cp.rho, cp.cfl, cp.final_time,
         cp.dx, cp.dy, cp.nu, cp.dt, cp.omega, cp.tol_factor, cp.abs_tol, cp.max_iters, cp.total_steps,
         cp.print_interval, cp.save_interval, cp.h_inlet, cp.step_x, cp.step_i, cp.inlet_jmax, check_every, chunk,
-        _lib.ORDER[ordering], sweeps_per_launch)
+        _lib.ORDER[ordering], sweeps_per_launch, cp.ra, cp.pr, cp.kappa, cp.buoyancy, cp.t_hot, cp.t_cold,
+        cp.t_ref, cp.t_perturb)
 
 
 class _SolverBase:
@@ -202,7 +203,27 @@ class BackwardsStepSolver(_SolverBase):
     COLLECTION = "backwards_step_animation.pvd"
 
 
-SOLVERS = {CAVITY: CavitySolver, CHANNEL: ChannelSolver, BACKSTEP: BackwardsStepSolver}
+class RayleighBenardSolver(_SolverBase):
+    """BASELINE configs[4] (no reference solver): the cavity's projection step
+    with the lid at rest plus a Boussinesq temperature field."""
+    CASE = RAYLEIGH_BENARD
+    VTK_BASE = "rayleigh_benard"
+    COLLECTION = "rayleigh_benard_animation.pvd"
+
+    def advanceTemperature(self) -> None:
+        _lib.check(_lib.lib().cfd_advance_temperature(self._h), "advanceTemperature")
+
+    def nusselt(self) -> float:
+        """Mean wall-normal conductive flux at the hot wall over dT/H (one-sided)."""
+        T = self.field("t")
+        p = self.params
+        if self.owned_rows()[0] != 1:
+            raise ValueError("nusselt() needs the bottom wall (rank owning row 1)")
+        return float(np.mean((p.t_hot - T[1, 1:-1]) / (0.5 * p.dy)) / (p.t_hot - p.t_cold))
+
+
+SOLVERS = {CAVITY: CavitySolver, CHANNEL: ChannelSolver, BACKSTEP: BackwardsStepSolver,
+           RAYLEIGH_BENARD: RayleighBenardSolver}
 
 
 def solver_for(params: CaseParams, **kw) -> _SolverBase:
@@ -227,6 +248,13 @@ def write_vtk_arrays(params: CaseParams, filename: str, time_value: float, uc: n
     ptrs = [a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) for a in arrs]
     _lib.check(_lib.lib().cfd_write_vtk_arrays(ctypes.byref(cp), filename.encode(), time_value, *ptrs),
                "write_structured_grid")
+
+
+def params_from_library_rb(ra: float, pr: float, nx: int = 0, ny: int = 0, dt: float = 0.0) -> _lib.CfdParams:
+    """The C++ Rayleigh-Benard derivation (cfd_params_init_rb)."""
+    out = _lib.CfdParams()
+    _lib.check(_lib.lib().cfd_params_init_rb(ra, pr, nx, ny, dt, ctypes.byref(out)), "cfd_params_init_rb")
+    return out
 
 
 def params_from_library(case: int, re: float = 0.0, nx: int = 0, ny: int = 0, dt: float = 0.0) -> _lib.CfdParams:

@@ -52,6 +52,8 @@ struct Coef {
   double cav_corr;         // cavity: (dt/h) * rho           (cavity-01.cpp:696,701)
   double open_cu, open_cv; // open:   dt/(rho*dx), dt/(rho*dy) (channel-01.cpp:697,701)
   double tol_factor, abs_tol;
+  // Rayleigh-Benard (runs as case CAVITY with the lid at rest, plus T)
+  double kappa, buoy, t_hot, t_cold, t_ref;
 };
 
 // Control block for one Poisson solve (device memory).
@@ -253,6 +255,51 @@ __global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const dou
     const bool valid = !step || is_fluid(c, nx, ny, j, i) || is_fluid(c, nx, ny, j + 1, i);
     vs[o] = valid ? val : 0.0;
   }
+}
+
+// ------------------------------------------------------ Rayleigh-Benard --
+// No reference solver (BASELINE configs[4]); restated in oracle/cfd_oracle.c
+// (orc_temperature_bc, orc_thermal), bit-exact with it.
+
+// Temperature ghosts: hot bottom / cold top by reflection (like the lid,
+// cavity-01.cpp:523-529), adiabatic sides by copy; owned rows only.
+__global__ void bc_temperature_kernel(Geo g, Coef c, double* __restrict__ T) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nx = g.nx, ny = g.ny;
+  const int i = t + 1;
+  if (i <= nx) {
+    if (g.wj0 == 0) T[at(g, 0, i)] = 2.0 * c.t_hot - T[at(g, 1, i)];
+    if (g.wj1 == ny + 1) T[at(g, ny + 1, i)] = 2.0 * c.t_cold - T[at(g, ny, i)];
+  }
+  const int j = g.j0 + t;
+  if (j <= g.j1) {
+    T[at(g, j, 0)] = T[at(g, j, 1)];
+    T[at(g, j, nx + 1)] = T[at(g, j, nx)];
+  }
+}
+
+// One fused pass per cell: Boussinesq buoyancy on the v* face above it and
+// the explicit central advection-diffusion update of T (face fluxes with the
+// step's starting velocities). HBM-bound: reads T (5-point, rows reused via
+// L2), u, v, v*; writes T2, v*.
+__global__ __launch_bounds__(256) void thermal_kernel(Geo g, Coef c, const double* __restrict__ u,
+                                                      const double* __restrict__ v, const double* __restrict__ T,
+                                                      double* __restrict__ T2, double* __restrict__ vs) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int nx = g.nx, ny = g.ny;
+  if (j > g.j1 || i < 1 || i > nx) return;
+  const size_t o = at(g, j, i);
+  const size_t P = (size_t)g.pitch;
+  const double cc = T[o];
+  const double tE = T[o + 1], tW = T[o - 1], tN = T[o + P], tS = T[o - P];
+  if (j <= ny - 1) vs[o] = vs[o] + c.dt * (c.buoy * (0.5 * (cc + tN) - c.t_ref));
+  const double diff = c.kappa * ((tE - 2.0 * cc + tW) * c.idx2 + (tN - 2.0 * cc + tS) * c.idy2);
+  const double fe = u[o] * (0.5 * (cc + tE));
+  const double fw = u[o - 1] * (0.5 * (tW + cc));
+  const double fn = v[o] * (0.5 * (cc + tN));
+  const double fs = v[o - P] * (0.5 * (tS + cc));
+  T2[o] = cc + c.dt * (diff - (fe - fw) * c.idx - (fn - fs) * c.idy);
 }
 
 // --------------------------------------------------------------- source --

@@ -51,6 +51,8 @@ extern "C" int cfd_params_init(int case_id, double re, int nx, int ny, double dt
       p.cfl = 0.2; p.final_time = 15.0; p.tol_factor = 1e-7; p.abs_tol = 1e-10; p.max_iters = 10000;
       p.print_interval = 10; p.save_interval = 10; p.h_inlet = 1.0; p.step_x = 2.0;
       break;
+    case CFD_RAYLEIGH_BENARD:
+      return cfd_params_init_rb(re, 0.71, nx, ny, dt, out);
     default:
       cfd::set_last_error("unknown case_id");
       return CFD_E_ARG;
@@ -93,6 +95,55 @@ extern "C" int cfd_params_init(int case_id, double re, int nx, int ny, double dt
     cfd::set_last_error("Computed time step is non-positive. Check physical parameters!");
     return CFD_E_ARG;
   }
+  *out = p;
+  return CFD_OK;
+}
+
+// Rayleigh-Benard (BASELINE configs[4]; no reference solver, mirrors
+// cfd_amd/params.py): free-fall units, H = 1, L = nx/ny, lid at rest.
+extern "C" int cfd_params_init_rb(double ra, double pr, int nx, int ny, double dt, cfd_params* out) {
+  if (!out) {
+    cfd::set_last_error("null output");
+    return CFD_E_ARG;
+  }
+  cfd_params p;
+  std::memset(&p, 0, sizeof p);
+  p.case_id = CFD_RAYLEIGH_BENARD;
+  p.check_every = 1;
+  p.ordering = CFD_ORDER_RB;
+  p.nx = nx > 0 ? nx : 256;
+  p.ny = ny > 0 ? ny : 64;
+  p.ra = ra > 0 ? ra : 1e6;
+  p.pr = pr > 0 ? pr : 0.71;
+  if (p.nx < 2 || p.ny < 2) {
+    cfd::set_last_error("grid must have at least 2 interior cells per direction");
+    return CFD_E_ARG;
+  }
+  p.height = 1.0;
+  p.length = p.nx * p.height / p.ny;
+  p.re = std::sqrt(p.ra / p.pr);
+  p.u_ref = 0.0;
+  p.rho = 1.0;
+  p.cfl = 0.5;
+  p.final_time = 100.0;
+  p.tol_factor = 1e-9;
+  p.abs_tol = 0.0;
+  p.max_iters = 10000;
+  p.print_interval = 100;
+  p.save_interval = 100;
+  p.nu = std::sqrt(p.pr / p.ra);
+  p.kappa = 1.0 / std::sqrt(p.ra * p.pr);
+  p.buoyancy = 1.0;
+  p.t_hot = 1.0;
+  p.t_cold = 0.0;
+  p.t_ref = 0.5 * (p.t_hot + p.t_cold);
+  p.t_perturb = 0.01;
+  p.dx = p.dy = p.length / p.nx;
+  const double h = p.dx;
+  p.dt = dt > 0 ? dt : p.cfl * std::min(0.25 * h * h / std::max(p.nu, p.kappa), h / 1.0);
+  p.omega = omega_2d(p.nx, p.ny);
+  p.total_steps = (int)(p.final_time / p.dt);
+  p.inlet_jmax = p.ny;
   *out = p;
   return CFD_OK;
 }

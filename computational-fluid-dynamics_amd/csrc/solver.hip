@@ -34,7 +34,7 @@ static void check_launch(const char* what) {
   if (e != hipSuccess) throw Error(CFD_E_DEVICE, std::string("launch ") + what + ": " + hipGetErrorString(e));
 }
 
-enum { B_P0 = 0, B_P1, B_F, B_US, B_VS, B_U, B_V, B_UC, B_VC, B_PL, B_P2, NB };  // B_PL: lex-mode initial field;
+enum { B_P0 = 0, B_P1, B_F, B_US, B_VS, B_U, B_V, B_UC, B_VC, B_PL, B_P2, B_T, B_T2, NB };  // B_T/B_T2: Rayleigh-Benard only;  // B_PL: lex-mode initial field;
 // B_P2: third pressure buffer of the lagged convergence test (ranks)
 static int pbuf(int idx) { return idx == 0 ? B_P0 : idx == 1 ? B_P1 : B_P2; }
 
@@ -76,6 +76,11 @@ static Coef make_coef(const cfd_params& p) {
   c.open_cv = p.dt / (p.rho * p.dy);
   c.tol_factor = p.tol_factor;
   c.abs_tol = p.abs_tol;
+  c.kappa = p.kappa;
+  c.buoy = p.buoyancy;
+  c.t_hot = p.t_hot;
+  c.t_cold = p.t_cold;
+  c.t_ref = p.t_ref;
   return c;
 }
 
@@ -140,8 +145,20 @@ class Solver {
   int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order
   int march_min_th = MARCH_MIN_TH;
 
+  // Rayleigh-Benard: the cavity's projection (P.case_id is set to CFD_CAVITY,
+  // u_ref 0 = lid at rest) plus the temperature stage on tcur/tnext.
+  bool thermal = false;
+  int tcur = B_T, tnext = B_T2;
+
   Solver(const cfd_params& p, int device, const std::vector<std::pair<int, int>>& rows, Comm* cm)
       : P(p), dev(device), comm(cm) {
+    if (P.case_id == CFD_RAYLEIGH_BENARD) {
+      thermal = true;
+      if (!(P.kappa > 0)) throw Error(CFD_E_ARG, "Rayleigh-Benard needs kappa > 0");
+      if (std::fabs(P.dx - P.dy) > 1e-12 * P.dx) throw Error(CFD_E_ARG, "Rayleigh-Benard needs dx == dy");
+      P.case_id = CFD_CAVITY;
+      P.u_ref = 0.0;
+    }
     validate();
     C = make_coef(P);
     if (const char* kv = std::getenv("CFD_POISSON_KERNEL")) {
@@ -194,6 +211,7 @@ class Solver {
       g.nrows = (j1 - j0 + 1) + 2 * HALO;
       const size_t n = (size_t)g.nrows * (size_t)pitch;
       for (int k = 0; k < NB; ++k) {
+        if ((k == B_T || k == B_T2) && !thermal) continue;
         HIPC(hipMalloc(&s.b[k], n * sizeof(double)));
         HIPC(hipMemsetAsync(s.b[k], 0, n * sizeof(double), st));
       }
@@ -239,7 +257,45 @@ class Solver {
     fluid_count = (double)((long long)P.nx * P.ny - solid);
     // channel-01.cpp:352 / backwards_step-01.cpp:396: constructor applies the velocity BCs
     if (P.case_id != CFD_CAVITY) apply_bc(false);
+    if (thermal) init_temperature();
     HIPC(hipStreamSynchronize(st));
+  }
+
+  // Initial temperature (oracle/cfd_oracle.c orc_create): conduction profile
+  // plus one roll's perturbation, set on the host once like the reference's
+  // field initialisation, then uploaded.
+  void init_temperature() {
+    int rows, cols, first, last;
+    field_dims(CFD_FIELD_T, rows, cols);
+    owned_field_rows(CFD_FIELD_T, first, last);
+    std::vector<double> h((size_t)(last - first + 1) * cols, 0.0);
+    const double pi = 3.14159265358979323846;
+    const double length = P.length;
+    for (int j = std::max(first, 1); j <= std::min(last, P.ny); ++j)
+      for (int i = 1; i <= P.nx; ++i) {
+        const double x = (i - 0.5) * P.dx, y = (j - 0.5) * P.dy;
+        h[(size_t)(j - first) * cols + i] =
+            P.t_hot + (P.t_cold - P.t_hot) * y + P.t_perturb * std::sin(pi * y) * std::cos(pi * x / length);
+      }
+    transfer(CFD_FIELD_T, nullptr, h.data(), h.size());
+  }
+
+  // Rayleigh-Benard stage (oracle orc_temperature_bc + orc_thermal): ghosts,
+  // halo rows, then the fused buoyancy + advection-diffusion kernel. Needs the
+  // u/v halos compute_tentative() exchanged.
+  void advance_temperature() {
+    if (!thermal) throw Error(CFD_E_STATE, "cfd_advance_temperature: not a Rayleigh-Benard solver");
+    for (auto& s : S) {
+      const int n = std::max(P.nx, s.g.j1 - s.g.j0 + 1);
+      bc_temperature_kernel<<<(n + 255) / 256, 256, 0, st>>>(s.g, C, s.b[tcur]);
+      check_launch("bc_temperature");
+    }
+    if (multi()) exchange(tcur, 1);
+    for (auto& s : S) {
+      thermal_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_U], s.b[B_V], s.b[tcur], s.b[tnext], s.b[B_VS]);
+      check_launch("thermal");
+    }
+    std::swap(tcur, tnext);
   }
 
   ~Solver() {
@@ -782,6 +838,7 @@ class Solver {
     if (P.case_id == CFD_CAVITY) {
       apply_bc(false);
       compute_tentative();
+      if (thermal) advance_temperature();
       build_source();
       solve(out);
       correct();
@@ -836,6 +893,9 @@ class Solver {
       case CFD_FIELD_V: return B_V;
       case CFD_FIELD_UC: return B_UC;
       case CFD_FIELD_VC: return B_VC;
+      case CFD_FIELD_T:
+        if (thermal) return tcur;
+        break;
     }
     throw Error(CFD_E_ARG, "unknown field");
   }
@@ -965,6 +1025,7 @@ int cfd_destroy(cfd_solver* s) {
 int cfd_apply_bc(cfd_solver* s) { return guard([&] { S_(s)->apply_bc(false); }); }
 int cfd_apply_tentative_bc(cfd_solver* s) { return guard([&] { S_(s)->apply_bc(true); }); }
 int cfd_compute_tentative(cfd_solver* s) { return guard([&] { S_(s)->compute_tentative(); }); }
+int cfd_advance_temperature(cfd_solver* s) { return guard([&] { S_(s)->advance_temperature(); }); }
 int cfd_build_source(cfd_solver* s) { return guard([&] { S_(s)->build_source(); }); }
 int cfd_solve_pressure(cfd_solver* s, cfd_step_info* out) { return guard([&] { S_(s)->solve(out); }); }
 int cfd_apply_correction(cfd_solver* s) { return guard([&] { S_(s)->correct(); }); }

@@ -20,9 +20,12 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 2
+#define CFD_AMD_ABI_VERSION 3
 
-enum cfd_case { CFD_CAVITY = 0, CFD_CHANNEL = 1, CFD_BACKSTEP = 2 };
+/* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
+ * tree (only figures): it is the cavity's projection step with a resting lid
+ * plus a Boussinesq temperature field; see DESIGN.md §5c ("parity unpinned"). */
+enum cfd_case { CFD_CAVITY = 0, CFD_CHANNEL = 1, CFD_BACKSTEP = 2, CFD_RAYLEIGH_BENARD = 3 };
 
 /* Fields, named after the reference members (cavity-01.cpp:336-344). */
 enum cfd_field {
@@ -33,7 +36,8 @@ enum cfd_field {
   CFD_FIELD_U = 5,    /* u_corrected         (ny+2) x (nx+1) */
   CFD_FIELD_V = 6,    /* v_corrected         (ny+1) x (nx+2) */
   CFD_FIELD_UC = 7,   /* u_center            (ny+2) x (nx+2) */
-  CFD_FIELD_VC = 8    /* v_center            (ny+2) x (nx+2) */
+  CFD_FIELD_VC = 8,   /* v_center            (ny+2) x (nx+2) */
+  CFD_FIELD_T = 9     /* temperature (Rayleigh-Benard only) (ny+2) x (nx+2) */
 };
 
 enum {
@@ -68,6 +72,11 @@ typedef struct cfd_params {
                            (the reference's sweep order, bit-identical; one device, one strip) */
   int sweeps_per_launch; /* red-black SOR iterations fused into one kernel launch: 0 = auto (3 for
                            the cavity, 2 otherwise), 1, 2 or 3 (cavity); bit-identical either way */
+  /* Rayleigh-Benard (case 3), free-fall units: H = 1, U = sqrt(g beta dT H),
+   * nu = sqrt(Pr/Ra), kappa = 1/sqrt(Ra Pr); hot bottom wall t_hot, cold top
+   * wall t_cold, adiabatic side walls; buoyancy (T - t_ref) on v. */
+  double ra, pr, kappa, buoyancy, t_hot, t_cold, t_ref;
+  double t_perturb;     /* initial T = conduction profile + t_perturb*sin(pi y)cos(pi x/L) */
 } cfd_params;
 
 enum cfd_ordering { CFD_ORDER_RB = 0, CFD_ORDER_LEX = 1 };
@@ -103,6 +112,11 @@ const char* cfd_last_error(void);
  * (cavity-01.cpp:355-364, channel-01.cpp:336-345, backwards_step-01.cpp:377-388). */
 int cfd_params_init(int case_id, double re, int nx, int ny, double dt, cfd_params* out);
 
+/* Rayleigh-Benard parameters (no reference counterpart; BASELINE configs[4]):
+ * Ra, Pr, grid (aspect L = nx/ny, H = 1, dx = dy), dt (<= 0: CFL-derived).
+ * cfd_params_init(CFD_RAYLEIGH_BENARD, ra, nx, ny, dt, out) = this with Pr 0.71. */
+int cfd_params_init_rb(double ra, double pr, int nx, int ny, double dt, cfd_params* out);
+
 /* Construct a solver: CavitySolver()/ChannelSolver()/BackwardsStepSolver()
  * (cavity-01.cpp:355, channel-01.cpp:336, backwards_step-01.cpp:377) —
  * allocateFields + setupGeometry + the initial applyBoundaryConditions of the
@@ -120,6 +134,10 @@ int cfd_destroy(cfd_solver* s);
 int cfd_apply_bc(cfd_solver* s);                  /* applyBoundaryConditions   cavity-01.cpp:523 / channel-01.cpp:509 */
 int cfd_apply_tentative_bc(cfd_solver* s);        /* applyVelocityBC(u*,v*)    channel-01.cpp:369 */
 int cfd_compute_tentative(cfd_solver* s);         /* computeTentativeVelocities cavity-01.cpp:548 */
+/* Rayleigh-Benard only: temperature ghost cells, buoyancy added to v* and one
+ * explicit advection-diffusion update of T (fused kernel); cfd_step runs it
+ * between cfd_compute_tentative and cfd_build_source. */
+int cfd_advance_temperature(cfd_solver* s);
 int cfd_build_source(cfd_solver* s);              /* source term (+ mean removal) cavity-01.cpp:622 / channel-01.cpp:608 */
 int cfd_solve_pressure(cfd_solver* s, cfd_step_info* out); /* solverPressurePoisson cavity-01.cpp:609 */
 int cfd_apply_correction(cfd_solver* s);          /* applyPressureCorrection   cavity-01.cpp:695 */

@@ -26,6 +26,8 @@ struct orc_state {
 };
 
 #define AT(a, j, i) ((a)[(size_t)(j) * (size_t)W + (size_t)(i)])
+/* Rayleigh-Benard runs the cavity's projection (all no-slip walls, lid at rest) */
+#define CAVLIKE(s) ((s)->P.case_id == ORC_CAVITY || (s)->P.case_id == ORC_RBC)
 
 double orc_omega_square(int n) {
   /* cavity-01.cpp:74-78 */
@@ -69,6 +71,17 @@ orc_state* orc_create(const orc_params* p) {
       cnt += fl;
     }
   s->fluid_count = cnt;
+  if (p->case_id == ORC_RBC) {
+    /* conduction profile between the walls plus one roll's perturbation,
+     * cell centres x = (i - 1/2) dx, y = (j - 1/2) dy, H = 1 */
+    const double pi = 3.14159265358979323846;
+    double* T = s->f[ORC_F_T];
+    for (int j = 1; j <= p->ny; ++j)
+      for (int i = 1; i <= p->nx; ++i) {
+        const double x = (i - 0.5) * p->dx, y = (j - 0.5) * p->dy;
+        AT(T, j, i) = p->t_hot + (p->t_cold - p->t_hot) * y + p->t_perturb * sin(pi * y) * cos(pi * x / p->length);
+      }
+  }
   return s;
 }
 
@@ -126,7 +139,7 @@ static void bc_open(orc_state* s, double* u, double* v) {
 }
 
 void orc_velocity_bc(orc_state* s, int tentative) {
-  if (s->P.case_id == ORC_CAVITY) { bc_cavity(s); return; }
+  if (CAVLIKE(s)) { bc_cavity(s); return; }
   if (tentative) bc_open(s, s->f[ORC_F_US], s->f[ORC_F_VS]);
   else bc_open(s, s->f[ORC_F_U], s->f[ORC_F_V]);
 }
@@ -190,7 +203,7 @@ double orc_source(orc_state* s) {
   const double* vs = s->f[ORC_F_VS];
   double* f = s->f[ORC_F_SRC];
   double max_source = 0.0;
-  if (s->P.case_id == ORC_CAVITY) {
+  if (CAVLIKE(s)) {
     /* cavity-01.cpp:613-630 (inside solverPressurePoisson) */
     const double inv = 1.0 / s->P.dx;
     const double dt_inv = 1.0 / s->P.dt;
@@ -327,7 +340,7 @@ static double sor_iteration(orc_state* s, int ordering) {
   double* p = s->f[ORC_F_P];
   const double* f = s->f[ORC_F_SRC];
   const double omega = s->P.omega;
-  if (s->P.case_id == ORC_CAVITY) {
+  if (CAVLIKE(s)) {
     const double h = s->P.dx;
     if (ordering == ORC_LEX) {
       for (int j = 1; j <= ny; ++j)
@@ -365,7 +378,7 @@ static double sor_iteration(orc_state* s, int ordering) {
 static double solve_tolerance(orc_state* s, double* initial) {
   const int W = s->W, nx = s->P.nx, ny = s->P.ny;
   const double* f = s->f[ORC_F_SRC];
-  if (s->P.case_id == ORC_CAVITY) {
+  if (CAVLIKE(s)) {
     /* cavity-01.cpp:617-632: tolerance = factor * max|source|, loop primed with 1.0 */
     double m = 0.0;
     for (int j = 1; j <= ny; ++j)
@@ -387,7 +400,7 @@ static double solve_tolerance(orc_state* s, double* initial) {
 }
 
 void orc_poisson(orc_state* s, int ordering, int* iters, double* residual) {
-  if (s->P.case_id == ORC_CAVITY) {
+  if (CAVLIKE(s)) {
     /* cavity-01.cpp:610-611: every solve starts from a zero field */
     const size_t n = (size_t)(s->P.ny + 2) * (size_t)(s->P.nx + 2);
     memset(s->f[ORC_F_P], 0, n * sizeof(double));
@@ -420,7 +433,7 @@ void orc_correct(orc_state* s) {
   double* u = s->f[ORC_F_U];
   double* v = s->f[ORC_F_V];
   const double rho = s->P.rho, dt = s->P.dt;
-  if (s->P.case_id == ORC_CAVITY) {
+  if (CAVLIKE(s)) {
     /* cavity-01.cpp:695-711 */
     const double dt_over_h = dt / s->P.dx;
     for (int j = 1; j <= ny; ++j)
@@ -489,7 +502,7 @@ void orc_stats(orc_state* s, double* max_div, double* avg_ke) {
         ke += 0.5 * (AT(uc, j, i) * AT(uc, j, i) + AT(vc, j, i) * AT(vc, j, i));
         cnt++;
       }
-  if (s->P.case_id == ORC_CAVITY) {
+  if (CAVLIKE(s)) {
     const double inv = 1.0 / s->P.dx;
     for (int j = 1; j <= ny; ++j)
       for (int i = 1; i <= nx; ++i) {
@@ -510,9 +523,79 @@ void orc_stats(orc_state* s, double* max_div, double* avg_ke) {
   *max_div = md;
 }
 
+/* ------------------------------------------------- Rayleigh-Benard ---- */
+
+void orc_temperature_bc(orc_state* s) {
+  /* Dirichlet walls by ghost reflection (as the lid, cavity-01.cpp:523-529):
+   * hot bottom, cold top; adiabatic sides by ghost copy. Corners unused. */
+  const int W = s->W, nx = s->P.nx, ny = s->P.ny;
+  double* T = s->f[ORC_F_T];
+  for (int i = 1; i <= nx; ++i) {
+    AT(T, 0, i) = 2.0 * s->P.t_hot - AT(T, 1, i);
+    AT(T, ny + 1, i) = 2.0 * s->P.t_cold - AT(T, ny, i);
+  }
+  for (int j = 1; j <= ny; ++j) {
+    AT(T, j, 0) = AT(T, j, 1);
+    AT(T, j, nx + 1) = AT(T, j, nx);
+  }
+}
+
+void orc_thermal(orc_state* s) {
+  /* Boussinesq buoyancy on the v faces, then explicit central advection-
+   * diffusion of T with the velocities of the step's start (u_corrected after
+   * the wall BCs), conservative face fluxes as in the momentum predictor
+   * (cavity-01.cpp:548-603). */
+  const int W = s->W, nx = s->P.nx, ny = s->P.ny;
+  const double idx = 1.0 / s->P.dx, idy = 1.0 / s->P.dy;
+  const double idx2 = 1.0 / (s->P.dx * s->P.dx), idy2 = 1.0 / (s->P.dy * s->P.dy);
+  const double dt = s->P.dt, kap = s->P.kappa, b = s->P.buoyancy, tr = s->P.t_ref;
+  const double* u = s->f[ORC_F_U];
+  const double* v = s->f[ORC_F_V];
+  const double* T = s->f[ORC_F_T];
+  double* vs = s->f[ORC_F_VS];
+  double* T2 = s->f[ORC_F_T2];
+  for (int j = 1; j <= ny - 1; ++j)
+    for (int i = 1; i <= nx; ++i) AT(vs, j, i) = AT(vs, j, i) + dt * (b * (0.5 * (AT(T, j, i) + AT(T, j + 1, i)) - tr));
+  for (int j = 1; j <= ny; ++j)
+    for (int i = 1; i <= nx; ++i) {
+      const double c = AT(T, j, i);
+      const double diff = kap * ((AT(T, j, i + 1) - 2.0 * c + AT(T, j, i - 1)) * idx2 +
+                                 (AT(T, j + 1, i) - 2.0 * c + AT(T, j - 1, i)) * idy2);
+      const double fe = AT(u, j, i) * (0.5 * (c + AT(T, j, i + 1)));
+      const double fw = AT(u, j, i - 1) * (0.5 * (AT(T, j, i - 1) + c));
+      const double fn = AT(v, j, i) * (0.5 * (c + AT(T, j + 1, i)));
+      const double fs = AT(v, j - 1, i) * (0.5 * (AT(T, j - 1, i) + c));
+      AT(T2, j, i) = c + dt * (diff - (fe - fw) * idx - (fn - fs) * idy);
+    }
+  double* t = s->f[ORC_F_T];
+  s->f[ORC_F_T] = s->f[ORC_F_T2];
+  s->f[ORC_F_T2] = t;
+}
+
+double orc_nusselt(orc_state* s) {
+  /* Nu = <-dT/dy>_bottom / ((t_hot - t_cold) / H), one-sided at the wall */
+  const int W = s->W, nx = s->P.nx;
+  const double* T = s->f[ORC_F_T];
+  double q = 0.0;
+  for (int i = 1; i <= nx; ++i) q += (s->P.t_hot - AT(T, 1, i)) / (0.5 * s->P.dy);
+  return q / nx / (s->P.t_hot - s->P.t_cold);
+}
+
 /* ------------------------------------------------------------ timestep -- */
 
 void orc_step(orc_state* s, int ordering, int* iters, double* residual) {
+  if (s->P.case_id == ORC_RBC) {
+    /* the cavity's order (cavity-01.cpp:387-390) with the thermal stage
+     * between predictor and source */
+    orc_velocity_bc(s, 0);
+    orc_temperature_bc(s);
+    orc_tentative(s);
+    orc_thermal(s);
+    orc_source(s);
+    orc_poisson(s, ordering, iters, residual);
+    orc_correct(s);
+    return;
+  }
   if (s->P.case_id == ORC_CAVITY) {
     /* cavity-01.cpp:387-390 */
     orc_velocity_bc(s, 0);

@@ -15,9 +15,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 LEX, RB = 0, 1
-F_P, F_SRC, F_RES, F_US, F_VS, F_U, F_V, F_UC, F_VC = range(9)
+F_P, F_SRC, F_RES, F_US, F_VS, F_U, F_V, F_UC, F_VC, F_T, F_T2 = range(11)
 FIELD_IDS = {"p": F_P, "src": F_SRC, "res": F_RES, "us": F_US, "vs": F_VS, "u": F_U, "v": F_V, "uc": F_UC,
-             "vc": F_VC}
+             "vc": F_VC, "t": F_T}
 
 
 class OrcParams(ctypes.Structure):
@@ -27,6 +27,9 @@ class OrcParams(ctypes.Structure):
         ("u_ref", ctypes.c_double), ("dt", ctypes.c_double), ("omega", ctypes.c_double),
         ("tol_factor", ctypes.c_double), ("abs_tol", ctypes.c_double), ("max_iters", ctypes.c_int),
         ("step_i", ctypes.c_int), ("inlet_jmax", ctypes.c_int),
+        ("kappa", ctypes.c_double), ("buoyancy", ctypes.c_double), ("t_hot", ctypes.c_double),
+        ("t_cold", ctypes.c_double), ("t_ref", ctypes.c_double), ("t_perturb", ctypes.c_double),
+        ("length", ctypes.c_double),
     ]
 
 
@@ -61,6 +64,10 @@ def lib() -> ctypes.CDLL:
         L.orc_poisson_fixed.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, dp]
         L.orc_step.argtypes = [ctypes.c_void_p, ctypes.c_int, ip, dp]
         L.orc_stats.argtypes = [ctypes.c_void_p, dp, dp]
+        L.orc_temperature_bc.argtypes = [ctypes.c_void_p]
+        L.orc_thermal.argtypes = [ctypes.c_void_p]
+        L.orc_nusselt.restype = ctypes.c_double
+        L.orc_nusselt.argtypes = [ctypes.c_void_p]
         L.orc_omega_square.restype = ctypes.c_double
         L.orc_omega_square.argtypes = [ctypes.c_int]
         L.orc_omega_2d.restype = ctypes.c_double
@@ -72,7 +79,9 @@ def lib() -> ctypes.CDLL:
 def params_from_case(p) -> OrcParams:
     """Build oracle parameters from a cfd_amd.params.CaseParams."""
     return OrcParams(p.case_id, p.nx, p.ny, p.dx, p.dy, p.nu, p.rho, p.u_ref, p.dt, p.omega, p.tol_factor,
-                     p.abs_tol, p.max_iters, p.step_i, p.inlet_jmax)
+                     p.abs_tol, p.max_iters, p.step_i, p.inlet_jmax, getattr(p, "kappa", 0.0),
+                     getattr(p, "buoyancy", 0.0), getattr(p, "t_hot", 1.0), getattr(p, "t_cold", 0.0),
+                     getattr(p, "t_ref", 0.0), getattr(p, "t_perturb", 0.0), p.length)
 
 
 class Oracle:
@@ -132,6 +141,16 @@ class Oracle:
         md, ke = ctypes.c_double(), ctypes.c_double()
         lib().orc_stats(self.h, ctypes.byref(md), ctypes.byref(ke))
         return md.value, ke.value
+
+    # Rayleigh-Benard phases (case 3; parity unpinned: no reference solver)
+    def temperature_bc(self) -> None:
+        lib().orc_temperature_bc(self.h)
+
+    def thermal(self) -> None:
+        lib().orc_thermal(self.h)
+
+    def nusselt(self) -> float:
+        return lib().orc_nusselt(self.h)
 
     def step(self) -> tuple[int, float]:
         it, res = ctypes.c_int(), ctypes.c_double()

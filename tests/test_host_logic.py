@@ -44,7 +44,7 @@ def test_nm_exports_match_header():
 
 
 def test_abi_version():
-    assert _lib.lib().cfd_abi_version() == 2
+    assert _lib.lib().cfd_abi_version() == 3
 
 
 @pytest.mark.parametrize("case", ["cavity", "channel", "backwards_step"])
@@ -58,6 +58,44 @@ def test_params_python_equals_cpp(case, over):
     for f in ("nx", "ny", "dx", "dy", "nu", "dt", "omega", "total_steps", "step_i", "inlet_jmax", "max_iters",
               "tol_factor", "abs_tol", "print_interval", "save_interval", "height"):
         assert getattr(cp, f) == getattr(lp, f), f
+
+
+@pytest.mark.parametrize("over", [{}, {"nx": 128, "ny": 32}, {"nx": 8192, "ny": 2048, "ra": 1e6}, {"dt": 1e-3},
+                                  {"ra": 2e4, "pr": 7.0, "nx": 64, "ny": 16}])
+def test_rayleigh_benard_params_python_equals_cpp(over):
+    """BASELINE configs[4] (no reference solver): params.py == cfd_params_init_rb."""
+    cp = C.make_params("rayleigh_benard", **over)
+    lp = C.params_from_library_rb(over.get("ra", 1e6), over.get("pr", 0.71), over.get("nx", 0), over.get("ny", 0),
+                                  over.get("dt", 0.0))
+    for f in ("nx", "ny", "dx", "dy", "nu", "kappa", "buoyancy", "t_hot", "t_cold", "t_ref", "t_perturb", "dt",
+              "omega", "total_steps", "max_iters", "tol_factor", "abs_tol", "height", "length", "re", "ra", "pr",
+              "u_ref"):
+        assert getattr(cp, f) == getattr(lp, f), f
+    assert lp.case_id == C.RAYLEIGH_BENARD and lp.dx == lp.dy
+    # cfd_params_init(case 3, re=Ra) = the same derivation with Pr 0.71
+    if "pr" not in over:
+        lq = C.params_from_library(C.RAYLEIGH_BENARD, over.get("ra", 1e6), over.get("nx", 0), over.get("ny", 0),
+                                   over.get("dt", 0.0))
+        assert bytes(lq) == bytes(lp)
+
+
+def test_rayleigh_benard_oracle_onset():
+    """Oracle sanity (parity unpinned): the conduction state is linearly unstable
+    above Ra_c ~ 1708 (rigid walls) and stable below it."""
+    import oracle as O
+    ke = {}
+    for ra in (1e3, 2e4):
+        o = O.Oracle(C.make_params("rayleigh_benard", nx=32, ny=8, ra=ra, max_iters=400), ordering=O.RB)
+        k = []
+        for n in range(240):
+            o.step()
+            if n in (80, 239):
+                k.append(o.stats()[1])
+        ke[ra] = k
+        nu = o.nusselt()
+        assert 0.99 < nu < 1.2, nu
+    assert ke[1e3][1] < ke[1e3][0]
+    assert ke[2e4][1] > 2 * ke[2e4][0]
 
 
 def test_baseline_configs_derive():
