@@ -26,7 +26,7 @@ constexpr char BLUE[] = "\033[34m";
 constexpr char CYAN[] = "\033[36m";
 
 struct Options {
-  double re = 0, dt = 0, final_time = 0;
+  double re = 0, dt = 0, final_time = 0, ra = 0, pr = 0;
   int nx = 0, ny = 0, steps = -1, max_iters = 0, save = 0, print = 0, device = 0, strips = 1, check_every = 1;
   bool vtk = true;
   bool exact = false;
@@ -35,7 +35,7 @@ struct Options {
 
 inline void usage(const char* prog) {
   std::cerr << "usage: " << prog
-            << " [--Re R] [--Nx N] [--Ny N] [--dt DT] [--final-time T] [--steps K] [--max-iters N]\n"
+            << " [--Re R | --Ra RA --Pr PR] [--Nx N] [--Ny N] [--dt DT] [--final-time T] [--steps K] [--max-iters N]\n"
                "       [--save-interval N] [--print-interval N] [--output-dir DIR] [--no-vtk]\n"
                "       [--device D] [--strips S] [--check-every C] [--exact]\n"
                "  --exact: the reference's lexicographic SOR order (bit-identical output, one strip)\n";
@@ -53,6 +53,8 @@ inline Options parse(int argc, char** argv) {
       return argv[++k];
     };
     if (a == "--Re") o.re = std::atof(next());
+    else if (a == "--Ra") o.ra = std::atof(next());
+    else if (a == "--Pr") o.pr = std::atof(next());
     else if (a == "--Nx") o.nx = std::atoi(next());
     else if (a == "--Ny") o.ny = std::atoi(next());
     else if (a == "--dt") o.dt = std::atof(next());
@@ -93,7 +95,12 @@ inline std::string frame_name(const std::string& base, int step) {
 inline int run_case(int case_id, int argc, char** argv) {
   const Options o = parse(argc, argv);
   cfd_params p;
-  if (cfd_params_init(case_id, o.re, o.nx, o.ny, o.dt, &p) != CFD_OK) die("parameters");
+  const bool rb = case_id == CFD_RAYLEIGH_BENARD;
+  if (rb) {
+    if (cfd_params_init_rb(o.ra, o.pr, o.nx, o.ny, o.dt, &p) != CFD_OK) die("parameters");
+  } else if (cfd_params_init(case_id, o.re, o.nx, o.ny, o.dt, &p) != CFD_OK) {
+    die("parameters");
+  }
   if (o.final_time > 0) {
     p.final_time = o.final_time;
     p.total_steps = (int)(p.final_time / p.dt);
@@ -104,7 +111,10 @@ inline int run_case(int case_id, int argc, char** argv) {
   p.check_every = o.check_every;
   if (o.exact) p.ordering = CFD_ORDER_LEX;
   const int total = o.steps >= 0 ? o.steps : p.total_steps;
-  const char* base = case_id == CFD_CAVITY ? "cavity_flow" : case_id == CFD_CHANNEL ? "channel_flow" : "backwards_step";
+  const char* base = case_id == CFD_CAVITY    ? "cavity_flow"
+                     : case_id == CFD_CHANNEL ? "channel_flow"
+                     : rb                     ? "rayleigh_benard"
+                                              : "backwards_step";
   const std::string coll = std::string(base) + (case_id == CFD_BACKSTEP ? "_animation.pvd" : "_animation.pvd");
 
   if (case_id == CFD_BACKSTEP) {
@@ -123,7 +133,12 @@ inline int run_case(int case_id, int argc, char** argv) {
   }
   std::cout << std::fixed << std::setprecision(6);
   std::cout << CYAN;
-  if (case_id == CFD_CAVITY) {
+  if (rb) {
+    std::cout << "=== Rayleigh-Benard Convection Simulation ===\n"
+              << "Domain: " << p.length << "x" << p.height << "\n"
+              << "Grid: " << p.nx << "x" << p.ny << " (spacing=" << p.dx << ")\n"
+              << "Rayleigh=" << p.ra << ", Prandtl=" << p.pr << ", thermal diffusivity=" << p.kappa << "\n";
+  } else if (case_id == CFD_CAVITY) {
     std::cout << "=== Lid-Driven Cavity Flow Simulation ===\n"
               << "Domain: " << p.length << "x" << p.height << "\n"
               << "Grid: " << p.nx << "x" << p.ny << " (spacing=" << p.dx << ")\n";
@@ -160,7 +175,18 @@ inline int run_case(int case_id, int argc, char** argv) {
     if (k % p.print_interval == 0 || k == 0) std::cout << BLUE << "Exported VTK file: " << fn << RESET << "\n";
   };
 
-  if (case_id == CFD_CAVITY) {
+  // Nusselt number at the hot wall from the bottom interior row of T
+  std::vector<double> tfield;
+  auto nusselt = [&]() {
+    int rows = 0, cols = 0;
+    if (cfd_field_shape(s, CFD_FIELD_T, &rows, &cols) != CFD_OK) die("field_shape");
+    tfield.resize((size_t)rows * cols);
+    if (cfd_get_field(s, CFD_FIELD_T, tfield.data(), tfield.size()) != CFD_OK) die("get_field");
+    double q = 0;
+    for (int i = 1; i <= p.nx; ++i) q += (p.t_hot - tfield[(size_t)cols + i]) / (0.5 * p.dy);
+    return q / p.nx / (p.t_hot - p.t_cold);
+  };
+  if (case_id == CFD_CAVITY || rb) {
     std::cout << GREEN << "Starting simulation...\n" << RESET;
     if (cfd_apply_bc(s) != CFD_OK) die("applyBoundaryConditions");
     exportf(0, 0.0);
@@ -174,7 +200,7 @@ inline int run_case(int case_id, int argc, char** argv) {
     cfd_step_info info;
     if (cfd_step(s, &info) != CFD_OK) die("timestep");
     if (info.sor_iterations >= p.max_iters) {
-      if (case_id == CFD_CAVITY)
+      if (case_id == CFD_CAVITY || rb)
         std::cerr << "Warning: SOR solver did not converge in " << p.max_iters
                   << " iterations. Final residual: " << info.residual << "\n";
       else
@@ -183,7 +209,13 @@ inline int run_case(int case_id, int argc, char** argv) {
     if (k % p.print_interval == 0 || k == total) {
       cfd_stats st;
       if (cfd_compute_stats(s, &st) != CFD_OK) die("logStatistics");
-      if (case_id == CFD_CAVITY)
+      if (rb)
+        std::cout << "Step " << std::setw(6) << k << "/" << p.total_steps << " | t=" << std::fixed << std::setprecision(2)
+                  << std::setw(6) << t << " | max(div)=" << std::setprecision(2) << std::scientific << std::setw(10)
+                  << st.max_divergence << " | avg_KE=" << std::fixed << std::setprecision(6) << std::setw(10)
+                  << st.avg_kinetic_energy << " | Nu=" << std::setprecision(4) << nusselt()
+                  << " | SOR_iters=" << std::setw(4) << info.sor_iterations << "\n";
+      else if (case_id == CFD_CAVITY)
         std::cout << "Step " << std::setw(6) << k << "/" << p.total_steps << " | t=" << std::fixed << std::setprecision(2)
                   << std::setw(6) << t << " | max(div)=" << std::setprecision(2) << std::scientific << std::setw(10)
                   << st.max_divergence << " | avg_KE=" << std::fixed << std::setprecision(6) << std::setw(10)

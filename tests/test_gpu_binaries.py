@@ -55,3 +55,22 @@ def test_binary_cli_overrides(tmp_path):
     assert "Grid: 128x128 (spacing=0.007812)" in out
     assert "Time: dt=0.001000, steps=20000, final_time=20.000000" in out
     assert any(l.startswith("Step     20/20000") for l in out)
+
+
+def test_rayleigh_benard_binary_matches_oracle(tmp_path):
+    """bin/rayleigh_benard (configs[4], parity unpinned): its logged SOR
+    iteration counts and Nusselt numbers equal the oracle restatement's."""
+    import cfd_amd as C
+    import oracle as O
+    out, _ = run("rayleigh_benard", "--Ra", "5e4", "--Nx", "64", "--Ny", "16", "--steps", "300",
+                 "--print-interval", "100", "--max-iters", "2000", "--no-vtk", cwd=tmp_path)
+    assert "=== Rayleigh-Benard Convection Simulation ===" in out
+    steps = [l for l in out if l.startswith("Step ")]
+    assert len(steps) == 3
+    o = O.Oracle(C.make_params("rayleigh_benard", nx=64, ny=16, ra=5e4, max_iters=2000), ordering=O.RB)
+    for k in range(1, 301):
+        it, _ = o.step()
+        if k % 100 == 0:
+            line = steps[k // 100 - 1]
+            assert f"SOR_iters={it:4d}" in line, (line, it)
+            assert f"Nu={o.nusselt():.4f}" in line, (line, o.nusselt())
