@@ -168,7 +168,7 @@ class _SolverBase:
 
         if output_directory is not None:
             os.makedirs(output_directory, exist_ok=True)
-        if self.CASE == CAVITY:
+        if self.CASE in (CAVITY, RAYLEIGH_BENARD):
             self.applyBoundaryConditions()
         export(0, 0.0)
         for k in range(1, total + 1):
@@ -178,7 +178,8 @@ class _SolverBase:
                 print(warning_line(p.case_id, p.max_iters, res), file=err)
             if k % p.print_interval == 0 or k == total:
                 md, ke = self.statistics()
-                print(step_line(p.case_id, k, p.total_steps, t, md, ke, it, res), file=out)
+                nu = self.nusselt() if p.case_id == RAYLEIGH_BENARD else None
+                print(step_line(p.case_id, k, p.total_steps, t, md, ke, it, res, nu), file=out)
             if k % p.save_interval == 0 or k == total:
                 export(k, t)
         if output_directory is not None:

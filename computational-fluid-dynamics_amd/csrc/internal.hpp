@@ -52,7 +52,7 @@ void comm_allreduce_sum(Comm* c, double* buf, size_t count, void* stream);
 
 // VTK output (vtk.cpp). Arrays are (ny+2) x (nx+2) row-major host doubles.
 void write_vtk_arrays(const cfd_params& p, const std::string& filename, double time_value, const double* uc,
-                      const double* vc, const double* pr);
+                      const double* vc, const double* pr, const double* temp = nullptr);
 void write_pvd(const std::string& filename, const char* const* files, const double* times, int n);
 
 bool host_is_fluid(const cfd_params& p, int j, int i);

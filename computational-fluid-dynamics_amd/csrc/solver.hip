@@ -943,6 +943,14 @@ class Solver {
     transfer(CFD_FIELD_UC, uc.data(), nullptr, n);
     transfer(CFD_FIELD_VC, vc.data(), nullptr, n);
     transfer(CFD_FIELD_P, pr.data(), nullptr, n);
+    if (thermal) {
+      std::vector<double> tf(n);
+      transfer(CFD_FIELD_T, tf.data(), nullptr, n);
+      cfd_params q = P;
+      q.case_id = CFD_RAYLEIGH_BENARD;
+      write_vtk_arrays(q, fn, t, uc.data(), vc.data(), pr.data(), tf.data());
+      return;
+    }
     write_vtk_arrays(P, fn, t, uc.data(), vc.data(), pr.data());
   }
 };

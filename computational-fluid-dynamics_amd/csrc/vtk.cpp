@@ -37,21 +37,24 @@ struct Out {
 }  // namespace
 
 void write_vtk_arrays(const cfd_params& p, const std::string& filename, double t, const double* uc,
-                      const double* vc, const double* pr) {
+                      const double* vc, const double* pr, const double* temp) {
   const int nx = p.nx, ny = p.ny, W = nx + 2;
   auto A = [W](const double* a, int j, int i) { return a[(size_t)j * W + i]; };
   const bool step = p.case_id == CFD_BACKSTEP;
   Out o;
   o.s.reserve((size_t)nx * ny * 80 + 1024);
   o.lit("# vtk DataFile Version 3.0\n");
-  if (p.case_id == CFD_CAVITY) o.lit("Lid-Driven Cavity Flow Data - Time: ");
+  // Rayleigh-Benard frames: the cavity's layout and vorticity + a temperature field
+  const bool rb = p.case_id == CFD_RAYLEIGH_BENARD;
+  if (rb) o.lit("Rayleigh-Benard Convection Data - Time: ");
+  else if (p.case_id == CFD_CAVITY) o.lit("Lid-Driven Cavity Flow Data - Time: ");
   else if (p.case_id == CFD_CHANNEL) o.lit("Channel Flow Data - Time: ");
   else o.lit("Backwards Step Flow Data - Time: ");
   o.num(t);
   o.nl();
   o.lit("ASCII\nDATASET STRUCTURED_POINTS\n");
   o.lit(("DIMENSIONS " + std::to_string(nx) + " " + std::to_string(ny) + " 1\n").c_str());
-  const double dx = p.dx, dy = (p.case_id == CFD_CAVITY) ? p.dx : p.dy;
+  const double dx = p.dx, dy = (p.case_id == CFD_CAVITY || rb) ? p.dx : p.dy;
   o.lit("ORIGIN ");
   o.num(dx * 0.5);
   o.lit(" ");
@@ -100,8 +103,14 @@ void write_vtk_arrays(const cfd_params& p, const std::string& filename, double t
   for (int j = 1; j <= ny; ++j)
     for (int i = 1; i <= nx; ++i) { o.num((!step || host_is_fluid(p, j, i)) ? A(pr, j, i) : 0.0); o.nl(); }
 
+  if (rb && temp) {
+    o.lit("SCALARS temperature double 1\nLOOKUP_TABLE default\n");
+    for (int j = 1; j <= ny; ++j)
+      for (int i = 1; i <= nx; ++i) { o.num(A(temp, j, i)); o.nl(); }
+  }
+
   o.lit("SCALARS vorticity double 1\nLOOKUP_TABLE default\n");
-  if (p.case_id == CFD_CAVITY) {
+  if (p.case_id == CFD_CAVITY || rb) {
     // cavity-01.cpp:187-224
     const int n_x = nx, n_y = ny;
     const double dx_inv = 1.0 / p.dx;

@@ -74,3 +74,27 @@ def test_rayleigh_benard_binary_matches_oracle(tmp_path):
             line = steps[k // 100 - 1]
             assert f"SOR_iters={it:4d}" in line, (line, it)
             assert f"Nu={o.nusselt():.4f}" in line, (line, o.nusselt())
+
+
+def test_rayleigh_benard_python_run_matches_binary(tmp_path):
+    """RayleighBenardSolver.run() prints the binary's log and writes the same
+    frames (temperature included)."""
+    import io
+
+    import cfd_amd as C
+    out, _ = run("rayleigh_benard", "--Ra", "5e4", "--Nx", "64", "--Ny", "16", "--steps", "40",
+                 "--print-interval", "20", "--save-interval", "20", "--max-iters", "2000",
+                 "--output-dir", "bin_out", cwd=tmp_path)
+    cp = C.make_params("rayleigh_benard", nx=64, ny=16, ra=5e4, max_iters=2000)
+    cp.print_interval = cp.save_interval = 20
+    s = C.RayleighBenardSolver(cp)
+    buf = io.StringIO()
+    s.run(output_directory=str(tmp_path / "py_out"), out=buf, err=io.StringIO(), steps=40)
+    py_steps = [l for l in buf.getvalue().splitlines() if l.startswith("Step ")]
+    bin_steps = [l for l in out if l.startswith("Step ")]
+    assert py_steps == bin_steps and len(py_steps) == 2
+    for k in (0, 20, 40):
+        a = (tmp_path / "bin_out" / f"rayleigh_benard_{k:06d}.vtk").read_bytes()
+        b = (tmp_path / "py_out" / f"rayleigh_benard_{k:06d}.vtk").read_bytes()
+        assert b"SCALARS temperature double 1" in a and b"Rayleigh-Benard Convection Data" in a
+        assert a == b
