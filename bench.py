@@ -217,7 +217,7 @@ def main() -> int:
                 "effective_sweep_frac": round(effective / HBM_PEAK_GBS, 4),
             },
         }
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:  # the CPU leg is timed at N=1 only
             log("timing the CPU baseline ...")
             line["cpu_baseline"] = cpu_baseline(cp.nx, args.ny, args.cpu_seconds, args.case)
         print(json.dumps(line), flush=True)
