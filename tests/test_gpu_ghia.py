@@ -1,0 +1,61 @@
+"""Physics validation of the GPU cavity (BASELINE configs[0]: Re=100; run
+here at 64x64, dt=4e-3, since the reference's 1e-9 SOR tolerance costs ~1900
+sweeps per step even at steady state), the check the reference README names ("centerline validation vs.
+Ghia et al.", README.md:27): run from rest to steady state and compare the
+centerline profiles with Ghia, Ghia & Shin (1982), J. Comput. Phys. 48, 387,
+Tables I/II (Re=100 column). This is a published-data check, not a parity test
+(parity vs the reference algorithm is tests/test_gpu_parity.py); tolerance:
+max |deviation| <= 0.015 (lid-velocity units); measured on MI355X: u 0.0033,
+v 0.0088 (3000 steps in 84 s)."""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import cfd_amd as C  # noqa: E402
+
+# (y, u) on the vertical centerline x = 0.5
+GHIA_U = np.array([
+    (0.0000, 0.00000), (0.0547, -0.03717), (0.0625, -0.04192), (0.0703, -0.04775), (0.1016, -0.06434),
+    (0.1719, -0.10150), (0.2813, -0.15662), (0.4531, -0.21090), (0.5000, -0.20581), (0.6172, -0.13641),
+    (0.7344, 0.00332), (0.8516, 0.23151), (0.9531, 0.68717), (0.9609, 0.73722), (0.9688, 0.78871),
+    (0.9766, 0.84123), (1.0000, 1.00000)])
+# (x, v) on the horizontal centerline y = 0.5
+GHIA_V = np.array([
+    (0.0000, 0.00000), (0.0625, 0.09233), (0.0703, 0.10091), (0.0781, 0.10890), (0.0938, 0.12317),
+    (0.1563, 0.16077), (0.2266, 0.17507), (0.2344, 0.17527), (0.5000, 0.05454), (0.8047, -0.24533),
+    (0.8594, -0.22445), (0.9063, -0.16914), (0.9453, -0.10313), (0.9531, -0.08864), (0.9609, -0.07391),
+    (0.9688, -0.05906), (1.0000, 0.00000)])
+
+
+@pytest.mark.timeout(300)
+def test_cavity_re100_matches_ghia():
+    n = 64
+    cp = C.make_params("cavity", re=100.0, nx=n, ny=n, dt=4e-3)
+    s = C.solver_for(cp)
+    s.applyBoundaryConditions()
+    t0 = time.perf_counter()
+    steps = 3000  # t = 12: steady state
+    for k in range(steps):
+        s.step()
+        if k % 500 == 499:
+            print(f"ghia: step {k + 1}, {time.perf_counter() - t0:.1f} s", flush=True)
+    uc, vc = s.interpolateToCellCenters()
+    s.close()
+    print(f"ghia: {steps} steps in {time.perf_counter() - t0:.1f} s")
+    h = 1.0 / n
+    centres = (np.arange(1, n + 1) - 0.5) * h
+    # the x = 0.5 line lies between cell columns n/2 and n/2+1 (rows likewise)
+    u_line = 0.5 * (uc[1:n + 1, n // 2] + uc[1:n + 1, n // 2 + 1])
+    v_line = 0.5 * (vc[n // 2, 1:n + 1] + vc[n // 2 + 1, 1:n + 1])
+    y = np.concatenate(([0.0], centres, [1.0]))
+    u = np.concatenate(([0.0], u_line, [1.0]))
+    v = np.concatenate(([0.0], v_line, [0.0]))
+    du = np.abs(np.interp(GHIA_U[:, 0], y, u) - GHIA_U[:, 1]).max()
+    dv = np.abs(np.interp(GHIA_V[:, 0], y, v) - GHIA_V[:, 1]).max()
+    print(f"ghia: max|u - u_Ghia| = {du:.4f}, max|v - v_Ghia| = {dv:.4f}")
+    assert du <= 0.015 and dv <= 0.015, (du, dv)
