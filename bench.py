@@ -17,9 +17,16 @@ timed region; `achieved` = the 24 B/cell one launch must move / launch time,
 lexicographic SOR loop — the reference's loop restated in C — on a bounded
 sample of the same grid, rank 0 only).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--global-ny NY]
 For N > 1 launch with torch.distributed.run (one rank per GPU); halos and the
 residual all-reduce travel over RCCL inside libcfd_amd.so.
+
+Scaling modes (config.workload says which):
+  weak (default): every rank owns --ny rows (4096), global grid nx x (N*ny);
+  strong (--global-ny NY): the N ranks split one nx x NY grid (4096² at N=8:
+  512 rows per rank).
+The residual test runs every SOR iteration at every N (the reference's stop
+rule; check_every 1), so 1-GPU and N-GPU runs stop at the same iteration.
 """
 from __future__ import annotations
 
@@ -77,12 +84,15 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--nx", type=int, default=4096)
     ap.add_argument("--ny", type=int, default=4096, help="rows per GPU (weak scaling)")
+    ap.add_argument("--global-ny", type=int, default=0,
+                    help="strong scaling: the ranks split one grid of this many rows (0: weak scaling)")
     ap.add_argument("--re", type=float, default=1000.0)
     ap.add_argument("--case", default="cavity", choices=["cavity", "channel", "backwards_step", "rayleigh_benard"],
                     help="workload (the metric is quoted on the cavity; the others are extra measurements)")
     ap.add_argument("--ra", type=float, default=1e6, help="Rayleigh number (--case rayleigh_benard)")
     ap.add_argument("--max-iters", type=int, default=10000)
-    ap.add_argument("--check-every", type=int, default=0, help="residual test cadence (0: 1 on 1 GPU, 8 on >1)")
+    ap.add_argument("--check-every", type=int, default=1,
+                    help="residual test every N SOR iterations (1 = the reference's stop rule, at every GPU count)")
     ap.add_argument("--sweeps-per-launch", type=int, default=0,
                     help="red-black SOR iterations fused per kernel launch (0: auto = 3 for the cavity)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -106,16 +116,21 @@ def main() -> int:
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    check_every = args.check_every or (1 if world == 1 else 8)
+    check_every = max(1, args.check_every)
+    strong = args.global_ny > 0
+    ny_global = args.global_ny if strong else args.ny * world
     if args.case == "rayleigh_benard":  # BASELINE configs[4]: Pr 0.71, the Ra given
-        cp = C.make_params(args.case, ra=args.ra, nx=args.nx, ny=args.ny * world, max_iters=args.max_iters)
+        cp = C.make_params(args.case, ra=args.ra, nx=args.nx, ny=ny_global, max_iters=args.max_iters)
     else:
-        cp = C.make_params(args.case, re=args.re, nx=args.nx, ny=args.ny * world, max_iters=args.max_iters)
+        cp = C.make_params(args.case, re=args.re, nx=args.nx, ny=ny_global, max_iters=args.max_iters)
     comm = None
+    comm_info = None
     if world > 1:
-        from cfd_amd.dist import init_comm, weak_rows
+        from cfd_amd.dist import comm_info as _comm_info
+        from cfd_amd.dist import init_comm, strip_rows, weak_rows
         comm = init_comm(dist, rank, world, local_rank)
-        rows = weak_rows(rank, args.ny)
+        comm_info = _comm_info(comm)
+        rows = strip_rows(rank, world, ny_global) if strong else weak_rows(rank, args.ny)
         solver = C.solver_for(cp, device=local_rank, check_every=check_every, rank_rows=rows, comm=comm,
                               sweeps_per_launch=args.sweeps_per_launch)
     else:
@@ -136,10 +151,11 @@ def main() -> int:
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    iters = []
+    iters, resids = [], []
     for _ in range(args.steps):
-        it, _res = solver.step()
+        it, res = solver.step()
         iters.append(it)
+        resids.append(res)
     solver.synchronize()
     torch.cuda.synchronize()
     barrier()
@@ -176,6 +192,9 @@ def main() -> int:
                 traffic = None
         mlups = updates / elapsed / 1e6
         kcase = "cavity" if args.case == "rayleigh_benard" else args.case  # RB runs the cavity SOR kernel
+        rows_here = g1 - g0 + 1
+        per_gpu = (f"{cp.nx}x{rows_here} fp64 cells per GPU (global {cp.nx}x{cp.ny} split over {n_gpus} GPUs)"
+                   if strong else f"{cp.nx}x{args.ny} fp64 cells per GPU (global {cp.nx}x{cp.ny})")
         line = {
             "metric": METRIC,
             "value": round(mlups, 2),
@@ -185,21 +204,24 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
                 "workload": f"{WORKLOAD[args.case]} "
                             + (f"Ra={cp.ra:g} Pr={cp.pr:g}" if args.case == "rayleigh_benard" else f"Re={args.re:g}")
-                            + f", {cp.nx}x{args.ny} fp64 cells per GPU "
-                            f"(global {cp.nx}x{cp.ny}), reference SOR tolerance {cp.tol_factor:g}*max|src|, "
-                            f"cap {cp.max_iters} sweeps/step",
-                "nx": cp.nx, "ny_per_gpu": args.ny, "global_ny": cp.ny,
+                            + f", {per_gpu}, reference SOR tolerance {cp.tol_factor:g}*max|src|, "
+                            f"cap {cp.max_iters} sweeps/step, {'strong' if strong else 'weak'} scaling",
+                "nx": cp.nx, "ny_per_gpu": rows_here, "global_ny": cp.ny,
                 "parallelism": f"strip{n_gpus}", "check_every": check_every,
             },
+            "rccl_ranks": comm_info["nranks"] if comm_info else None,
+            "transport": (comm_info["transport"] if comm_info else "none (1 GPU)"),
             "steps_per_sec": round(args.steps / elapsed, 4),
             "sor_iterations_per_step": iters,
+            "sor_cap_hits": sum(1 for i in iters if i >= cp.max_iters),
+            "final_residual_per_step": [float(f"{r:.6e}") for r in resids],
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -219,7 +241,7 @@ def main() -> int:
         }
         if not args.no_cpu_baseline and world == 1:  # the CPU leg is timed at N=1 only
             log("timing the CPU baseline ...")
-            line["cpu_baseline"] = cpu_baseline(cp.nx, args.ny, args.cpu_seconds, args.case)
+            line["cpu_baseline"] = cpu_baseline(cp.nx, cp.ny, args.cpu_seconds, args.case)
         print(json.dumps(line), flush=True)
 
     solver.close()

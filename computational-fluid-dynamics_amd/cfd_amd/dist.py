@@ -55,6 +55,15 @@ def init_comm(dist, rank: int, world: int, device: int):
     return comm
 
 
+def comm_info(comm) -> dict:
+    """What the transport reports about itself (RCCL: ncclCommCount / ncclCommUserRank)."""
+    from . import _lib
+
+    n, r, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _lib.check(_lib.lib().cfd_comm_info(comm, ctypes.byref(n), ctypes.byref(r), ctypes.byref(t)), "cfd_comm_info")
+    return {"nranks": n.value, "rank": r.value, "transport": "rccl" if t.value == 0 else "loopback"}
+
+
 def max_over_ranks(dist, value: float) -> float:
     import torch
 

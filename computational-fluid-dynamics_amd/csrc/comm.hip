@@ -1,4 +1,4 @@
-// comm.cpp — RCCL transport for the multi-process strip decomposition.
+// comm.hip — RCCL transport for the multi-process strip decomposition.
 //
 // One process per GPU; each rank owns a strip of rows and exchanges its
 // boundary rows with the ranks above and below (point-to-point send/recv over
@@ -34,6 +34,8 @@ struct Rccl {
   ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                             hipStream_t) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
+  ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*CommUserRank)(const ncclComm_t, int*) = nullptr;
 };
 
 Rccl& rccl() {
@@ -55,6 +57,8 @@ Rccl& rccl() {
     r.Recv = reinterpret_cast<decltype(r.Recv)>(dlsym(r.h, "ncclRecv"));
     r.AllReduce = reinterpret_cast<decltype(r.AllReduce)>(dlsym(r.h, "ncclAllReduce"));
     r.GetErrorString = reinterpret_cast<decltype(r.GetErrorString)>(dlsym(r.h, "ncclGetErrorString"));
+    r.CommCount = reinterpret_cast<decltype(r.CommCount)>(dlsym(r.h, "ncclCommCount"));
+    r.CommUserRank = reinterpret_cast<decltype(r.CommUserRank)>(dlsym(r.h, "ncclCommUserRank"));
   });
   if (!r.h || !r.GetUniqueId || !r.CommInitRank || !r.Send || !r.Recv || !r.AllReduce || !r.GroupStart ||
       !r.GroupEnd)
@@ -94,6 +98,21 @@ Comm* comm_init(const unsigned char* id, int nranks, int rank, int device) {
   return cm;
 }
 
+void comm_info(Comm* c, int* nranks, int* rank, int* transport) {
+  if (!c) throw Error(CFD_E_ARG, "null communicator");
+  if (c->hub) {
+    *nranks = c->nranks;
+    *rank = c->rank;
+    *transport = 1;
+    return;
+  }
+  Rccl& r = rccl();
+  if (!r.CommCount || !r.CommUserRank) throw Error(CFD_E_COMM, "RCCL lacks ncclCommCount / ncclCommUserRank");
+  check(r.CommCount(static_cast<ncclComm_t>(c->nccl), nranks), "ncclCommCount");
+  check(r.CommUserRank(static_cast<ncclComm_t>(c->nccl), rank), "ncclCommUserRank");
+  *transport = 0;
+}
+
 void comm_destroy(Comm* c) {
   if (!c) return;
   if (c->hub) {
@@ -111,6 +130,8 @@ void comm_destroy(Comm* c) {
 // and live in separate host threads of one process (RCCL refuses two ranks on
 // one GPU). Only used to test the rank code path; copies are device-to-device
 // on the receiving rank's stream, ordered against the sender with events.
+
+constexpr int LOOP_MAX_RANKS = 32;
 
 struct LoopHub {
   int n;
@@ -142,7 +163,7 @@ struct LoopHub {
   } while (0)
 
 LoopHub* loop_hub_create(int nranks) {
-  if (nranks < 1) throw Error(CFD_E_ARG, "nranks must be >= 1");
+  if (nranks < 1 || nranks > LOOP_MAX_RANKS) throw Error(CFD_E_ARG, "loopback nranks must be in [1, 32]");
   return new LoopHub(nranks);
 }
 void loop_hub_destroy(LoopHub* h) { delete h; }
@@ -194,11 +215,18 @@ static void loop_group_end(Comm* c, hipStream_t st) {
   c->pending.clear();
 }
 
-__global__ void loop_reduce_kernel(double* const* bufs, int n, size_t count, int op, double* out) {
+struct LoopPtrs {
+  const double* p[LOOP_MAX_RANKS];
+};
+
+// Reduction over the ranks' buffers in rank order (a fixed order: every rank
+// computes the same bits). The pointer table travels by value in the kernel
+// arguments, so the all-reduce is stream-ordered like RCCL's: no host sync.
+__global__ void loop_reduce_kernel(LoopPtrs bufs, int n, size_t count, int op, double* out) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (i >= count) return;
-  double v = bufs[0][i];
-  for (int r = 1; r < n; ++r) v = op ? fmax(v, bufs[r][i]) : v + bufs[r][i];
+  double v = bufs.p[0][i];
+  for (int r = 1; r < n; ++r) v = op ? fmax(v, bufs.p[r][i]) : v + bufs.p[r][i];
   out[i] = v;
 }
 
@@ -206,8 +234,12 @@ static void loop_allreduce(Comm* c, double* buf, size_t count, int op, hipStream
   LoopHub& h = *c->hub;
   const int me = c->rank;
   if (c->tmp_count < count) {
-    if (c->tmp) LHIP(hipFree(c->tmp));
-    LHIP(hipMalloc(&c->tmp, count * sizeof(double) + h.n * sizeof(double*)));
+    // (a later, larger all-reduce reallocates: drain the stream's uses of the old scratch first)
+    if (c->tmp) {
+      LHIP(hipStreamSynchronize(st));
+      LHIP(hipFree(c->tmp));
+    }
+    LHIP(hipMalloc(&c->tmp, count * sizeof(double)));
     c->tmp_count = count;
   }
   LHIP(hipEventRecord((hipEvent_t)c->ev_ready, st));
@@ -215,10 +247,9 @@ static void loop_allreduce(Comm* c, double* buf, size_t count, int op, hipStream
   h.ready[me] = (hipEvent_t)c->ev_ready;
   h.barrier();
   for (int r = 0; r < h.n; ++r) LHIP(hipStreamWaitEvent(st, h.ready[r], 0));
-  double** dptrs = reinterpret_cast<double**>(c->tmp + count);
-  LHIP(hipMemcpyAsync(dptrs, h.bufs.data(), h.n * sizeof(double*), hipMemcpyHostToDevice, st));
-  LHIP(hipStreamSynchronize(st));  // (pointer table comes from host memory shared by all ranks)
-  loop_reduce_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(dptrs, h.n, count, op, c->tmp);
+  LoopPtrs tab{};
+  for (int r = 0; r < h.n; ++r) tab.p[r] = h.bufs[r];
+  loop_reduce_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(tab, h.n, count, op, c->tmp);
   LHIP(hipEventRecord((hipEvent_t)c->ev_done, st));
   h.done[me] = (hipEvent_t)c->ev_done;
   h.barrier();

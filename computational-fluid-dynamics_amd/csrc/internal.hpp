@@ -16,7 +16,7 @@ struct Error : std::runtime_error {
 
 void set_last_error(const std::string& msg);
 
-// RCCL transport (comm.cpp). Loaded with dlopen on first use so the
+// RCCL transport (comm.hip). Loaded with dlopen on first use so the
 // single-GPU library has no RCCL dependency.
 struct LoopHub;  // in-process transport (testing the rank path on one device)
 struct LoopOp {
@@ -43,6 +43,7 @@ LoopHub* loop_hub_create(int nranks);
 void loop_hub_destroy(LoopHub* h);
 Comm* comm_init_loopback(LoopHub* h, int rank, int device);
 void comm_destroy(Comm* c);
+void comm_info(Comm* c, int* nranks, int* rank, int* transport);
 void comm_group_start(Comm* c);
 void comm_group_end(Comm* c, void* stream);
 void comm_send(Comm* c, const double* buf, size_t count, int peer, void* stream);

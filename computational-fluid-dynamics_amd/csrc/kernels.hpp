@@ -386,19 +386,16 @@ __global__ void tol_kernel(Coef c, const double* __restrict__ srcmax, double* __
 
 // ------------------------------------------------------------- Poisson --
 //
-// One red-black SOR iteration of the reference's pressure equation, fused
-// into one launch: load a (BY+2H) x (BX+2H) tile of p and the matching f tile
-// into LDS, update red cells on tile+3, black cells on tile+2, refresh the
-// ghost / solid cells on tile+1 (channel-01.cpp:531-541,
-// backwards_step-01.cpp:685-740 — after the sweep, as the reference does),
-// then compute the max-norm residual on the tile and write it out. The
-// overlapping halos are recomputed redundantly, so one launch reads p and f
-// once and writes p once (24 B per cell) and the residual needs no second
-// pass. p_in / p_out ping-pong, so tiles never read a neighbour's new values.
+// Red-black SOR of the reference's pressure equation. Each launch reads p_in
+// and f once and writes p_out once (24 B per cell) for one or several fused
+// iterations (below); p_in / p_out ping-pong, so tiles never read a
+// neighbour's new values and overlapping halos are recomputed redundantly.
 //
 // SOR updates: cavity-01.cpp:643-654 (indicator form), channel-01.cpp:659-666
 // / backwards_step-01.cpp:900-909 (anisotropic form). Residuals:
 // cavity-01.cpp:659-677, channel-01.cpp:672-681, backwards_step-01.cpp:916-930.
+// Ghost / solid refresh after each sweep: channel-01.cpp:531-541,
+// backwards_step-01.cpp:685-740.
 
 template <int CASE>
 __device__ __forceinline__ double sor_update(const Coef& c, int nx, int ny, int j, int i, double pc, double pW,
@@ -442,193 +439,6 @@ __device__ __forceinline__ double residual_at(const Coef& c, int nx, int ny, int
   }
 }
 
-template <int CASE, int BX, int BY>
-struct PoissonTile {
-  static constexpr int H = (CASE == CAVITY) ? 3 : 4;  // cavity has no ghost refresh
-  static constexpr int LW = BX + 2 * H;
-  static constexpr int LH = BY + 2 * H;
-  static constexpr int FW = LW - 2;  // f on tile + (H-1)
-  static constexpr int FH = LH - 2;
-};
-
-template <int CASE, int BX, int BY>
-__global__ __launch_bounds__(256) void poisson_rbsor_kernel(Geo g, Coef c, const double* __restrict__ pin,
-                                                            double* __restrict__ pout,
-                                                            const double* __restrict__ f, PoissonCtl ctl,
-                                                            int k) {
-  using T = PoissonTile<CASE, BX, BY>;
-  constexpr int H = T::H, LW = T::LW, LH = T::LH, FW = T::FW, FH = T::FH;
-  constexpr int NT = 256;
-  __shared__ double sp[LH * LW];
-  __shared__ double sf[FH * FW];
-  __shared__ int s_active;
-
-  const int tid = threadIdx.x;
-  const int nx = g.nx, ny = g.ny;
-
-  // ---- convergence test of the previous iteration (reference loop condition) ----
-  if (tid < 64) {
-    const double tol = ctl.tol[0];
-    const bool stopped = ctl.stop[0] != 0;
-    const bool check = (k == 1) || ((k - 1) % ctl.check_every == 0);
-    bool active;
-    if (stopped) {
-      active = false;
-    } else if (!check) {
-      active = true;
-    } else {
-      double prev;
-      if (k == 1) {
-        prev = ctl.tol[1];
-      } else {
-        const double* slot = ctl.ring + (size_t)((k - 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-        prev = (tid < RES_SHARDS) ? slot[tid * SHARD_STRIDE] : 0.0;
-        prev = wave_max(prev);
-      }
-      active = prev > tol;
-      if (!active && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
-        ctl.stop[1] = k - 1;
-        ctl.stop[0] = 1;
-      }
-    }
-    if (tid == 0) s_active = active ? 1 : 0;
-  }
-  __syncthreads();
-  if (!s_active) return;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && tid < RES_SHARDS) {
-    // clear the slot iteration k+1 accumulates into (k-1's slot stays readable)
-    ctl.ring[(size_t)((k + 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + tid * SHARD_STRIDE] = 0.0;
-  }
-
-  const int ti0 = blockIdx.x * BX;            // global column of tile origin
-  const int tj0 = g.wj0 + blockIdx.y * BY;    // global row of tile origin
-  const int li0 = ti0 - H, lj0 = tj0 - H;     // global coords of LDS (0,0)
-  // rows that exist in storage and in the physical grid
-  const int rmin = max(g.row_lo, 0), rmax = min(g.row_lo + g.nrows - 1, ny + 1);
-
-  // ---- stage p (tile+H) and f (tile+H-1) in LDS ----
-  for (int e = tid; e < LH * LW; e += NT) {
-    const int r = e / LW, q = e - r * LW;
-    const int gj = lj0 + r, gi = li0 + q;
-    double val = 0.0;
-    if (gj >= rmin && gj <= rmax && gi >= 0 && gi <= nx + 1) val = pin[at(g, gj, gi)];
-    sp[e] = val;
-  }
-  for (int e = tid; e < FH * FW; e += NT) {
-    const int r = e / FW, q = e - r * FW;
-    const int gj = lj0 + 1 + r, gi = li0 + 1 + q;
-    double val = 0.0;
-    if (gj >= rmin && gj <= rmax && gi >= 0 && gi <= nx + 1) val = f[at(g, gj, gi)];
-    sf[e] = val;
-  }
-  __syncthreads();
-
-  // ---- red (color 0) on tile+H-1, black (color 1) on tile+H-2 ----
-#pragma unroll
-  for (int color = 0; color < 2; ++color) {
-    const int m = H - 1 - color;            // margin around the tile
-    const int rw = BX + 2 * m, rh = BY + 2 * m;
-    const int half = (rw + 1) / 2;
-    for (int e = tid; e < rh * half; e += NT) {
-      const int r = e / half, q = e - r * half;
-      const int gj = tj0 - m + r;
-      const int gstart = ti0 - m;
-      const int par = (color - gstart - gj) & 1;  // (gi + gj) & 1 == color
-      const int qq = par + 2 * q;
-      if (qq >= rw) continue;
-      const int gi = gstart + qq;
-      if (!is_fluid(c, nx, ny, gj, gi)) continue;
-      if (gj < rmin + 1 || gj > rmax - 1) continue;  // needs both vertical neighbours stored
-      const int lr = gj - lj0, lq = gi - li0;
-      const int o = lr * LW + lq;
-      const double fc = sf[(lr - 1) * FW + (lq - 1)];
-      sp[o] = sor_update<CASE>(c, nx, ny, gj, gi, sp[o], sp[o - 1], sp[o + 1], sp[o - LW], sp[o + LW], fc);
-    }
-    __syncthreads();
-  }
-
-  // ---- ghost / solid refresh on tile+1 (open cases) ----
-  if (CASE != CAVITY) {
-    constexpr int RW = BX + 2, RH = BY + 2;
-    constexpr int NR = (RW * RH + NT - 1) / NT;
-    // only tiles whose tile+1 region touches a ghost layer or the solid block
-    const bool touches = (ti0 - 1 <= 0) || (ti0 + BX >= nx + 1) || (tj0 - 1 <= 0) || (tj0 + BY >= ny + 1) ||
-                         (CASE == BACKSTEP && ti0 - 1 <= c.step_i && tj0 + BY >= c.inlet_jmax + 1);
-    if (touches) {
-      double nv[NR];
-      int no[NR];
-#pragma unroll
-      for (int s = 0; s < NR; ++s) {
-        no[s] = -1;
-        nv[s] = 0.0;
-        const int e = tid + s * NT;
-        if (e >= RW * RH) continue;
-        const int r = e / RW, q = e - r * RW;
-        const int gj = tj0 - 1 + r, gi = ti0 - 1 + q;
-        if (gj < rmin || gj > rmax || gi < 0 || gi > nx + 1) continue;
-        const int o = (gj - lj0) * LW + (gi - li0);
-        const bool jin = gj >= 1 && gj <= ny, iin = gi >= 1 && gi <= nx;
-        if (gi == 0 && jin) {
-          nv[s] = sp[o + 1]; no[s] = o;                 // inlet Neumann
-        } else if (gi == nx + 1 && jin) {
-          nv[s] = 0.0; no[s] = o;                       // outlet Dirichlet
-        } else if (gj == 0 && iin) {
-          nv[s] = sp[o + LW]; no[s] = o;                // bottom wall Neumann
-        } else if (gj == ny + 1 && iin) {
-          nv[s] = sp[o - LW]; no[s] = o;                // top wall Neumann
-        } else if (CASE == BACKSTEP && jin && iin && !is_fluid(c, nx, ny, gj, gi)) {
-          double sum = 0.0;
-          int n = 0;
-          if (gi > 1 && is_fluid(c, nx, ny, gj, gi - 1)) { sum += sp[o - 1]; n++; }
-          if (gi < nx && is_fluid(c, nx, ny, gj, gi + 1)) { sum += sp[o + 1]; n++; }
-          if (gj > 1 && is_fluid(c, nx, ny, gj - 1, gi)) { sum += sp[o - LW]; n++; }
-          if (gj < ny && is_fluid(c, nx, ny, gj + 1, gi)) { sum += sp[o + LW]; n++; }
-          if (n > 0) { nv[s] = sum / n; no[s] = o; }
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int s = 0; s < NR; ++s)
-        if (no[s] >= 0) sp[no[s]] = nv[s];
-    }
-    __syncthreads();
-  }
-
-  // ---- residual on the tile + write-out ----
-  double rmaxv = 0.0;
-  for (int e = tid; e < BY * BX; e += NT) {
-    const int r = e / BX, q = e - r * BX;
-    const int gj = tj0 + r, gi = ti0 + q;
-    if (gj > g.wj1 || gi > nx + 1) continue;
-    const int o = (gj - lj0) * LW + (gi - li0);
-    const double pc = sp[o];
-    pout[at(g, gj, gi)] = pc;
-    if (gj >= g.j0 && gj <= g.j1 && is_fluid(c, nx, ny, gj, gi)) {
-      const int lr = gj - lj0, lq = gi - li0;
-      const double fc = sf[(lr - 1) * FW + (lq - 1)];
-      const double rv = residual_at<CASE>(c, nx, ny, gj, gi, pc, sp[o - 1], sp[o + 1], sp[o - LW], sp[o + LW], fc);
-      rmaxv = fmax(rmaxv, fabs(rv));
-    }
-  }
-  double* slot = ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-  block_max_to_shard<NT>(rmaxv, slot, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
-}
-
-// ------------------------------------------------ Poisson, column march --
-//
-// The same red-black SOR iteration as poisson_rbsor_kernel (identical
-// arithmetic, bit-identical results), restructured for bandwidth: a block of
-// 256 threads owns 256 consecutive columns (248 output columns + 4 halo
-// columns each side) and marches down a band of TH rows. Each thread keeps a
-// 6-row register window of its column; row neighbours come from two LDS row
-// rings. At front row R one step does
-//   load p_in(R), f(R-1)      red at row R-1      black at row R-2
-//   ghost/solid refresh at row R-3 (open cases)   residual + store at row R-4
-// and every LDS value read in a step was written in an earlier step, so one
-// barrier per row suffices. Bands overlap by 4 rows (recomputed), tiles by 4
-// columns each side. HBM traffic per cell: p_in + f read once, p_out written
-// once (24 B) plus the band/tile overlap.
-
 template <int CASE>
 __device__ __forceinline__ bool refresh_value(const Coef& c, int nx, int ny, int gj, int gi, double self,
                                               double pW, double pE, double pS, double pN, double& out) {
@@ -652,178 +462,15 @@ __device__ __forceinline__ bool refresh_value(const Coef& c, int nx, int ny, int
   return false;
 }
 
-template <int CASE>
-__global__ __launch_bounds__(256) void poisson_march_kernel(Geo g, Coef c, const double* __restrict__ pin,
-                                                            double* __restrict__ pout,
-                                                            const double* __restrict__ f, PoissonCtl ctl, int k,
-                                                            int TH, int ctiles, int nbands, int flags) {
-  // flags bit 0: alternate the march direction of neighbouring bands
-  //       bit 1: XCD-aware tile order
-  constexpr int NT = 256, H = 4, TW = NT - 2 * H, NR = 4;
-  __shared__ double L[NR][NT];  // post-red/black values (pre-refresh)
-  __shared__ double F[NR][NT];  // final values (after refresh)
-  __shared__ int s_active;
-
-  const int t = threadIdx.x;
-  const int nx = g.nx, ny = g.ny;
-
-  if (t < 64) {
-    const double tol = ctl.tol[0];
-    const bool stopped = ctl.stop[0] != 0;
-    const bool check = (k == 1) || ((k - 1) % ctl.check_every == 0);
-    bool active;
-    if (stopped) {
-      active = false;
-    } else if (!check) {
-      active = true;
-    } else {
-      double prev;
-      if (k == 1) {
-        prev = ctl.tol[1];
-      } else {
-        const double* slot = ctl.ring + (size_t)((k - 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-        prev = (t < RES_SHARDS) ? slot[t * SHARD_STRIDE] : 0.0;
-        prev = wave_max(prev);
-      }
-      active = prev > tol;
-      if (!active && t == 0 && blockIdx.x == 0) {
-        ctl.stop[1] = k - 1;
-        ctl.stop[0] = 1;
-      }
-    }
-    if (t == 0) s_active = active ? 1 : 0;
-  }
-  __syncthreads();
-  if (!s_active) return;
-  if (blockIdx.x == 0 && t < RES_SHARDS)
-    ctl.ring[(size_t)((k + 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + t * SHARD_STRIDE] = 0.0;
-
-  // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin dispatch),
-  // so consecutive tile ids -- vertically adjacent bands of one column tile --
-  // are given to blocks on one XCD and read their shared halo rows from its L2.
-  const int nb = ctiles * nbands;
-  const int L8 = (nb / 8) * 8;
-  const int bl = (int)blockIdx.x;
-  const int tile = ((flags & 2) && bl < L8) ? (bl % 8) * (nb / 8) + bl / 8 : bl;
-  const int band = tile % nbands, ctile = tile / nbands;
-
-  const int gi = ctile * TW - H + t;
-  const int y0 = g.wj0 + band * TH;
-  const int y1 = min(y0 + TH, g.wj1 + 1);  // one past the last output row
-  if (y0 > g.wj1) return;                  // (uniform) empty band
-  const bool col_ok = gi >= 0 && gi <= nx + 1;
-  const bool icol = gi >= 1 && gi <= nx;
-  const bool out_col = col_ok && t >= H && t < NT - H;
-  const bool edge = (t == 0) || (t == NT - 1);
-  const bool upd_col = icol && !edge;
-  const bool step_open_col = (CASE != BACKSTEP) || (gi > c.step_i);  // fluid in every interior row
-  const int rmin = max(g.row_lo, 0), rmax = min(g.row_lo + g.nrows - 1, ny + 1);
-  const size_t P = (size_t)g.pitch;
-  // alternate march direction: a band's shared halo rows are read by both
-  // neighbours at the same time (both at their start, or both at their end)
-  const int d = ((flags & 1) && (band & 1)) ? -1 : 1;
-  const int Rbeg = (d > 0) ? y0 - H : y1 - 1 + H;
-  const int nsteps = (y1 - y0) + 2 * H;
-
-  auto fluid = [&](int j) -> bool {  // is_fluid(c, nx, ny, j, gi) with the column part hoisted
-    return icol && j >= 1 && j <= ny && (CASE != BACKSTEP || step_open_col || j <= c.inlet_jmax);
-  };
-  auto row_ok = [&](int R) -> bool { return col_ok && R >= rmin && R <= rmax; };
-  const double* prow = pin + (ptrdiff_t)(Rbeg - g.row_lo) * (ptrdiff_t)P + gi;
-  const double* frow = f + (ptrdiff_t)(Rbeg - d - g.row_lo) * (ptrdiff_t)P + gi;
-  const ptrdiff_t dP = (ptrdiff_t)d * (ptrdiff_t)P;
-
-  // register windows (march order): w<k> = post-black value of row R-(5-k)d,
-  // q<k> = final value of row R-(5-k)d; f of rows R-4d .. R-d
-  double w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
-  double q0 = 0, q1 = 0, q2 = 0;
-  double fa = 0, fb = 0, fc = 0, fd = 0;
-  double rmaxv = 0.0;
-
-  // prefetch queue: 3 rows of p_in and f in flight
-  double np1 = row_ok(Rbeg) ? prow[0] : 0.0, nf1 = row_ok(Rbeg - d) ? frow[0] : 0.0;
-  double np2 = row_ok(Rbeg + d) ? prow[dP] : 0.0, nf2 = row_ok(Rbeg) ? frow[dP] : 0.0;
-  double np3 = row_ok(Rbeg + 2 * d) ? prow[2 * dP] : 0.0, nf3 = row_ok(Rbeg + d) ? frow[2 * dP] : 0.0;
-  prow += 3 * dP;
-  frow += 3 * dP;
-
-  int R = Rbeg;
-  for (int s = 0; s < nsteps; ++s, R += d) {
-    const double pR = np1, fR = nf1;
-    np1 = np2;
-    nf1 = nf2;
-    np2 = np3;
-    nf2 = nf3;
-    np3 = row_ok(R + 3 * d) ? prow[0] : 0.0;
-    nf3 = row_ok(R + 2 * d) ? frow[0] : 0.0;
-    prow += dP;
-    frow += dP;
-    w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = pR;
-    fa = fb; fb = fc; fc = fd; fd = fR;
-    L[R & (NR - 1)][t] = pR;
-
-    // red (color 0) at row R-d: neighbours along the march w3 (behind), w5 (ahead)
-    {
-      const int j = R - d;
-      if (upd_col && ((gi + j) & 1) == 0 && fluid(j) && j > rmin && j < rmax) {
-        const double pW = L[j & (NR - 1)][t - 1], pE = L[j & (NR - 1)][t + 1];
-        const double pS = (d > 0) ? w3 : w5, pN = (d > 0) ? w5 : w3;
-        w4 = sor_update<CASE>(c, nx, ny, j, gi, w4, pW, pE, pS, pN, fd);
-        L[j & (NR - 1)][t] = w4;
-      }
-    }
-    // black (color 1) at row R-2d: w2 (behind), w4 (ahead, red-updated)
-    {
-      const int j = R - 2 * d;
-      if (upd_col && ((gi + j) & 1) == 1 && fluid(j) && j > rmin && j < rmax) {
-        const double pW = L[j & (NR - 1)][t - 1], pE = L[j & (NR - 1)][t + 1];
-        const double pS = (d > 0) ? w2 : w4, pN = (d > 0) ? w4 : w2;
-        w3 = sor_update<CASE>(c, nx, ny, j, gi, w3, pW, pE, pS, pN, fc);
-        L[j & (NR - 1)][t] = w3;
-      }
-    }
-    // refresh at row R-3d (pre-refresh neighbours: w1, w3 along the march, L[R-3d] across)
-    q0 = q1;
-    q1 = q2;
-    {
-      const int j = R - 3 * d;
-      double nv = w2;
-      if (CASE != CAVITY && !edge) {
-        double out;
-        const double pS = (d > 0) ? w1 : w3, pN = (d > 0) ? w3 : w1;
-        if (refresh_value<CASE>(c, nx, ny, j, gi, w2, L[j & (NR - 1)][t - 1], L[j & (NR - 1)][t + 1], pS, pN, out))
-          nv = out;
-      }
-      q2 = nv;
-      F[j & (NR - 1)][t] = nv;
-    }
-    // residual + store at row R-4d: q0 (behind), q2 (ahead); F[R-4d] across
-    {
-      const int j = R - 4 * d;
-      if (out_col && j >= y0 && j < y1) {
-        pout[(size_t)(j - g.row_lo) * P + gi] = q1;
-        if (j >= g.j0 && j <= g.j1 && fluid(j)) {
-          const double pW = F[j & (NR - 1)][t - 1], pE = F[j & (NR - 1)][t + 1];
-          const double pS = (d > 0) ? q0 : q2, pN = (d > 0) ? q2 : q0;
-          const double rv = residual_at<CASE>(c, nx, ny, j, gi, q1, pW, pE, pS, pN, fa);
-          rmaxv = fmax(rmaxv, fabs(rv));
-        }
-      }
-    }
-    __syncthreads();
-  }
-  double* slot = ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-  block_max_to_shard<NT>(rmaxv, slot, tile % RES_SHARDS);
-}
-
 // ---------------------------------------------- Poisson, wave march -----
 //
-// The same red-black SOR iteration again (bit-identical), with no LDS and no
-// barriers: every wave is an independent tile of 128 columns (2 per lane,
-// 16-byte loads and stores) marching down a band of rows, and row neighbours
-// across lanes move by DPP wave shifts. 4 columns each side are halo
-// (recomputed), so a wave writes 120 columns. Rows R+1..R+4 of p_in and f
-// are kept in flight in registers.
+// One red-black SOR iteration per launch with no LDS and no barriers: every
+// wave is an independent tile of 128 columns (2 per lane, 16-byte loads and
+// stores) marching down a band of rows, and row neighbours across lanes move
+// by DPP wave shifts. 4 columns each side are halo (recomputed), so a wave
+// writes 120 columns. At front row R one step loads p_in(R), f(R-1); updates
+// red at R-1, black at R-2; refreshes ghosts / solids at R-3; computes the
+// residual and stores at R-4. Rows R+1..R+4 of p_in and f are in flight.
 
 // bound_ctrl: the lane without a source (0 resp. 63) reads 0, with no
 // zero-initialised destination to merge into (one v_mov_dpp per dword)
@@ -857,127 +504,9 @@ __device__ __forceinline__ double residual_abs(const Coef& c, int nx, int ny, in
   }
 }
 
-template <int CASE, int DIR, int PD, bool COPY = false>
-__device__ __forceinline__ void wave_march(const Geo& g, const Coef& c, const double* __restrict__ pin,
-                                           double* __restrict__ pout, const double* __restrict__ f, int lane,
-                                           int gi, int y0, int y1, double& rmaxv) {
-  constexpr int H = 4;
-  const int nx = g.nx, ny = g.ny;
-  const int rmin = max(g.row_lo, 0), rmax = min(g.row_lo + g.nrows - 1, ny + 1);
-  const size_t P = (size_t)g.pitch;
-  const bool pair_ok = gi >= 0 && gi + 1 < g.pitch;  // both columns stored (pitch >= nx+3)
-  const bool out_lane = pair_ok && lane >= H / 2 && lane < 64 - H / 2;
-  const bool icol_a = gi >= 1 && gi <= nx, icol_b = gi + 1 >= 1 && gi + 1 <= nx;
-  const bool open_a = (CASE != BACKSTEP) || (gi > c.step_i), open_b = (CASE != BACKSTEP) || (gi + 1 > c.step_i);
-  const int gic = min(max(gi, 0), g.pitch - 2);  // clamped column: loads always hit valid memory
-  const int Rbeg = (DIR > 0) ? y0 - H : y1 - 1 + H;
-  const int nsteps = (y1 - y0) + 2 * H;
-  auto fl_a = [&](int j) -> bool { return icol_a && j >= 1 && j <= ny && (open_a || j <= c.inlet_jmax); };
-  auto fl_b = [&](int j) -> bool { return icol_b && j >= 1 && j <= ny && (open_b || j <= c.inlet_jmax); };
-  auto ld = [&](const double* base, int R) -> double2 {
-    const int Rc = min(max(R, rmin), rmax);
-    const double2 v = *reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * P + gic);
-    const bool ok = pair_ok && R >= rmin && R <= rmax;
-    return ok ? v : make_double2(0.0, 0.0);
-  };
-
-  // windows in march order (behind -> ahead): w1..w5 rows R-4d..R (post-black),
-  // q0..q2 rows R-5d..R-3d (final), fa..fd f of rows R-4d..R-d
-  double2 z = make_double2(0.0, 0.0);
-  double2 w1 = z, w2 = z, w3 = z, w4 = z, w5 = z, q0 = z, q1 = z, q2 = z, fa = z, fb = z, fc = z, fd = z;
-  // prefetch queue: rows R .. R+(PD-1)d of p_in and R-d .. R+(PD-2)d of f in flight
-  double2 np[PD], nf[PD];
-#pragma unroll
-  for (int q = 0; q < PD; ++q) {
-    np[q] = ld(pin, Rbeg + q * DIR);
-    nf[q] = ld(f, Rbeg + (q - 1) * DIR);
-  }
-
-  int R = Rbeg;
-  for (int s = 0; s < nsteps; ++s, R += DIR) {
-    const double2 pR = np[0], fR = nf[0];
-#pragma unroll
-    for (int q = 0; q + 1 < PD; ++q) {
-      np[q] = np[q + 1];
-      nf[q] = nf[q + 1];
-    }
-    np[PD - 1] = ld(pin, R + PD * DIR);
-    nf[PD - 1] = ld(f, R + (PD - 1) * DIR);
-    w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = pR;
-    fa = fb; fb = fc; fc = fd; fd = fR;
-    if (COPY) {  // diagnostic timing build: same traffic, no arithmetic (results are wrong)
-      const int j = R - 4 * DIR;
-      if (out_lane && j >= y0 && j < y1)
-        *reinterpret_cast<double2*>(pout + (size_t)(j - g.row_lo) * P + gi) =
-            make_double2(w1.x + fa.x, w1.y + fa.y);
-      rmaxv = 1.0e300;  // never "converges": fixed sweep count for timing
-      continue;
-    }
-    // along the march: "behind" = S for DIR > 0, N for DIR < 0
-#define CFD_S(b, a) ((DIR > 0) ? (b) : (a))
-#define CFD_N(b, a) ((DIR > 0) ? (a) : (b))
-    // red (color 0) at row j = R-d: slot a red iff j even (gi is even)
-    {
-      const int j = R - DIR;
-      const double Lb = dpp_from_left(w4.y), Ra = dpp_from_right(w4.x);
-      const bool rowok = j > rmin && j < rmax;
-      if ((j & 1) == 0) {
-        const double nv = sor_update<CASE>(c, nx, ny, j, gi, w4.x, Lb, w4.y, CFD_S(w3.x, w5.x), CFD_N(w3.x, w5.x), fd.x);
-        w4.x = (rowok && fl_a(j)) ? nv : w4.x;
-      } else {
-        const double nv =
-            sor_update<CASE>(c, nx, ny, j, gi + 1, w4.y, w4.x, Ra, CFD_S(w3.y, w5.y), CFD_N(w3.y, w5.y), fd.y);
-        w4.y = (rowok && fl_b(j)) ? nv : w4.y;
-      }
-    }
-    // black (color 1) at row j = R-2d: slot a black iff j odd
-    {
-      const int j = R - 2 * DIR;
-      const double Lb = dpp_from_left(w3.y), Ra = dpp_from_right(w3.x);
-      const bool rowok = j > rmin && j < rmax;
-      if ((j & 1) == 1) {
-        const double nv = sor_update<CASE>(c, nx, ny, j, gi, w3.x, Lb, w3.y, CFD_S(w2.x, w4.x), CFD_N(w2.x, w4.x), fc.x);
-        w3.x = (rowok && fl_a(j)) ? nv : w3.x;
-      } else {
-        const double nv =
-            sor_update<CASE>(c, nx, ny, j, gi + 1, w3.y, w3.x, Ra, CFD_S(w2.y, w4.y), CFD_N(w2.y, w4.y), fc.y);
-        w3.y = (rowok && fl_b(j)) ? nv : w3.y;
-      }
-    }
-    // ghost / solid refresh at row j = R-3d (pre-refresh neighbours)
-    q0 = q1;
-    q1 = q2;
-    q2 = w2;
-    if (CASE != CAVITY) {
-      const int j = R - 3 * DIR;
-      const double Lb = dpp_from_left(w2.y), Ra = dpp_from_right(w2.x);
-      double out;
-      if (refresh_value<CASE>(c, nx, ny, j, gi, w2.x, Lb, w2.y, CFD_S(w1.x, w3.x), CFD_N(w1.x, w3.x), out)) q2.x = out;
-      if (refresh_value<CASE>(c, nx, ny, j, gi + 1, w2.y, w2.x, Ra, CFD_S(w1.y, w3.y), CFD_N(w1.y, w3.y), out))
-        q2.y = out;
-    }
-    // residual + store at row j = R-4d
-    {
-      const int j = R - 4 * DIR;
-      const double Lb = dpp_from_left(q1.y), Ra = dpp_from_right(q1.x);
-      const bool jout = j >= y0 && j < y1;
-      if (out_lane && jout) *reinterpret_cast<double2*>(pout + (size_t)(j - g.row_lo) * P + gi) = q1;
-      const bool jres = jout && j >= g.j0 && j <= g.j1;
-      const double ra = residual_abs<CASE>(c, nx, ny, j, gi, q1.x, Lb, q1.y, CFD_S(q0.x, q2.x), CFD_N(q0.x, q2.x), fa.x);
-      const double rb =
-          residual_abs<CASE>(c, nx, ny, j, gi + 1, q1.y, q1.x, Ra, CFD_S(q0.y, q2.y), CFD_N(q0.y, q2.y), fa.y);
-      rmaxv = fmax(rmaxv, (out_lane && jres && fl_a(j)) ? ra : 0.0);
-      rmaxv = fmax(rmaxv, (out_lane && jres && fl_b(j)) ? rb : 0.0);
-    }
-#undef CFD_S
-#undef CFD_N
-  }
-}
-
-// Ring-window version of wave_march (the default): every window is a 5-slot
-// ring addressed with compile-time slots and the march is unrolled by 5, so
-// rows never move between registers (the shifting version spends ~50 moves
-// per row). Slot of the row x*d behind the front row R at rotation ROT:
+// Every window is a 5-slot ring addressed with compile-time slots and the
+// march is unrolled by 5, so rows never move between registers. Slot of the
+// row x*d behind the front row R at rotation ROT:
 #define CFD_SLOT(X) ((((ROT) + 4 - (X)) % 5 + 10) % 5)
 
 struct WaveRing {
@@ -1009,22 +538,6 @@ struct WaveCtx {
   __device__ double2 ld_fast(const double* base, int R) const {
     const int Rc = min(max(R, rmin), rmax);
     const double2* src = reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * (size_t)g.pitch + gi);
-#ifdef CFD_NT_LOAD
-    // rows no other band reads (outside both 14-row band overlaps): streamed
-    if (R >= y0 + 8 && R < y1 - 8) {
-      typedef double d2v __attribute__((ext_vector_type(2)));
-      const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(src));
-      return make_double2(v.x, v.y);
-    }
-#endif
-#ifdef CFD_NT_PIN
-    // p_in streamed (f, re-read by every launch, may then stay in the Infinity Cache)
-    if (base == pin) {
-      typedef double d2v __attribute__((ext_vector_type(2)));
-      const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(src));
-      return make_double2(v.x, v.y);
-    }
-#endif
     return *src;
   }
 };

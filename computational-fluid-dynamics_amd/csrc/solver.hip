@@ -38,8 +38,7 @@ enum { B_P0 = 0, B_P1, B_F, B_US, B_VS, B_U, B_V, B_UC, B_VC, B_PL, B_P2, B_T, B
 // B_P2: third pressure buffer of the lagged convergence test (ranks)
 static int pbuf(int idx) { return idx == 0 ? B_P0 : idx == 1 ? B_P1 : B_P2; }
 
-constexpr int PBX = 64, PBY = 32;  // Poisson tile (fused-tile variant)
-constexpr int MARCH_MIN_TH = 24;   // minimum rows per band (column-march variant)
+constexpr int MARCH_MIN_TH = 24;   // minimum rows per band of a wave-march launch
 constexpr int OVL_ROWS = 16;       // rows next to each neighbour updated by the overlapped boundary launch
 
 struct Strip {
@@ -103,6 +102,8 @@ class Solver {
   int* h_stat = nullptr;    // pinned: 2 x {stop, iter}
   double* h_shard = nullptr;  // pinned: RES_SHARDS*SHARD_STRIDE
   hipEvent_t ev_poll[2] = {}, ev_a = nullptr, ev_b = nullptr;
+  hipEvent_t ev_s0 = nullptr, ev_s1 = nullptr;  // around the last whole timestep (cfd_timing.step_ms)
+  bool step_timed = false;                      // ev_s0/ev_s1 hold a step not yet added to T.step_ms
   // Halo overlap on ranks (RCCL): the rows next to the neighbours and the
   // exchange run on st_b while the interior rows run on st.
   hipStream_t st_b = nullptr;
@@ -114,10 +115,9 @@ class Solver {
   // and output of the pair a late stop lands in intact.
   bool lagged() const { return overlap && sweeps_per_launch() >= 2; }
   // red-black iterations per SOR launch: 3 for the cavity (its depth-7
-  // pipeline fits the 8-row halos), 2 for the open cases, 1 on request or for
-  // the legacy kernel variants
+  // pipeline fits the 8-row halos), 2 for the open cases, 1 on request
   int sweeps_per_launch() const {
-    if (kernel_variant != 0 || P.sweeps_per_launch == 1) return 1;
+    if (P.sweeps_per_launch == 1) return 1;
     if (P.sweeps_per_launch == 2) return 2;
     return P.case_id == CFD_CAVITY ? 3 : 2;
   }
@@ -137,11 +137,9 @@ class Solver {
   int last_bnd = 0;         // ev_bnd slot recorded last
   long long n_overlapped = 0;  // overlapped pair launches enqueued (this solve)
   cfd_timing T{};
-  int kernel_variant = 0;  // 0: wave march (default), 1: fused LDS tile, 2: block column march
   int resident_waves = 2048;  // wave-march tiles in flight (CUs x 4 SIMDs x waves per SIMD)
   int resident_pair_waves = 2048;  // the same for the two-iteration kernel
   int pair_edge_pct = 45;          // boundary-column band length, % of the interior march (swept, cavity triples: 40-47 best)
-  int resident_blocks = 1024;  // march-kernel blocks resident at once on this device
   int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order
   int march_min_th = MARCH_MIN_TH;
 
@@ -152,6 +150,15 @@ class Solver {
 
   Solver(const cfd_params& p, int device, const std::vector<std::pair<int, int>>& rows, Comm* cm)
       : P(p), dev(device), comm(cm) {
+    try {
+      init(rows);
+    } catch (...) {
+      release();  // whatever the failed construction allocated so far
+      throw;
+    }
+  }
+
+  void init(const std::vector<std::pair<int, int>>& rows) {
     if (P.case_id == CFD_RAYLEIGH_BENARD) {
       thermal = true;
       if (!(P.kappa > 0)) throw Error(CFD_E_ARG, "Rayleigh-Benard needs kappa > 0");
@@ -161,10 +168,6 @@ class Solver {
     }
     validate();
     C = make_coef(P);
-    if (const char* kv = std::getenv("CFD_POISSON_KERNEL")) {
-      const std::string v(kv);
-      kernel_variant = (v == "tile") ? 1 : (v == "march") ? 2 : 0;
-    }
     HIPC(hipSetDevice(dev));
     hipDeviceProp_t prop;
     HIPC(hipGetDeviceProperties(&prop, dev));
@@ -172,11 +175,6 @@ class Solver {
       throw Error(CFD_E_DEVICE, std::string("libcfd_amd requires gfx950 (MI355X); device is ") + prop.gcnArchName);
     HIPC(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     {
-      int per_cu = 0;
-      HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, poisson_march_kernel<CAVITY>, 256, 0));
-      if (const char* e = std::getenv("CFD_MARCH_BLOCKS_PER_CU")) per_cu = std::atoi(e);
-      resident_blocks = std::max(1, per_cu) * prop.multiProcessorCount;
-      if (const char* e = std::getenv("CFD_MARCH_FLAGS")) march_flags = std::atoi(e);
       int wps = 0;  // waves per SIMD of the wave-march kernel (1 block of 4 waves = 1 wave per SIMD)
       HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&wps, poisson_wave_kernel<CAVITY>, 256, 0));
       wps = std::max(1, std::min(wps, 4));
@@ -193,12 +191,12 @@ class Solver {
       if (const char* e = std::getenv("CFD_PAIR_WPS")) pps = std::max(1, std::atoi(e));
       if (const char* e = std::getenv("CFD_PAIR_EDGE_PCT")) pair_edge_pct = std::max(10, std::min(100, std::atoi(e)));
       resident_pair_waves = pps * 4 * prop.multiProcessorCount;
-      if (const char* e = std::getenv("CFD_MARCH_MIN_TH")) march_min_th = std::max(8, std::atoi(e));
     }
     pitch = ((P.nx + 3) + 15) / 16 * 16;  // >= nx+3: column pairs (gi, gi+1) stay inside a row
     size_t part = 0;
     for (auto [j0, j1] : rows) {
-      Strip s;
+      S.emplace_back();  // owned by the solver before its buffers exist (release() frees them)
+      Strip& s = S.back();
       Geo& g = s.g;
       g.nx = P.nx;
       g.ny = P.ny;
@@ -218,7 +216,6 @@ class Solver {
       s.grid2d = dim3((P.nx + 2 + 63) / 64, (j1 - j0 + 1 + 3) / 4);
       s.part_off = part;
       part += (size_t)s.grid2d.x * s.grid2d.y;
-      S.push_back(s);
     }
     npart = part;
     const size_t ringn = (size_t)RING * RES_SHARDS * SHARD_STRIDE;
@@ -237,6 +234,8 @@ class Solver {
     for (auto& e : ev_poll) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPC(hipEventCreate(&ev_a));
     HIPC(hipEventCreate(&ev_b));
+    HIPC(hipEventCreate(&ev_s0));
+    HIPC(hipEventCreate(&ev_s1));
     if (comm && comm->nranks > 1 && S.size() == 1) {
       const Geo& g0 = S[0].g;
       const char* e = std::getenv("CFD_OVERLAP");
@@ -298,20 +297,31 @@ class Solver {
     std::swap(tcur, tnext);
   }
 
-  ~Solver() {
+  ~Solver() { release(); }
+
+  // Frees everything; both streams are drained before any buffer they may
+  // still touch is released. Safe on a partly constructed solver.
+  void release() noexcept {
     (void)hipSetDevice(dev);
+    if (st_b) (void)hipStreamSynchronize(st_b);
     if (st) (void)hipStreamSynchronize(st);
     for (auto& s : S)
-      for (auto* p : s.b) (void)hipFree(p);
-    for (double* p : {ring, srcmax, divmax, tolv, total, partials}) (void)hipFree(p);
-    (void)hipFree(stop);
-    (void)hipHostFree(h_stat);
-    (void)hipHostFree(h_shard);
+      for (auto* p : s.b)
+        if (p) (void)hipFree(p);
+    S.clear();
+    for (double* p : {ring, srcmax, divmax, tolv, total, partials})
+      if (p) (void)hipFree(p);
+    ring = srcmax = divmax = tolv = total = partials = nullptr;
+    if (stop) (void)hipFree(stop);
+    stop = nullptr;
+    if (h_stat) (void)hipHostFree(h_stat);
+    if (h_shard) (void)hipHostFree(h_shard);
+    h_stat = nullptr;
+    h_shard = nullptr;
     for (auto& e : ev_poll)
       if (e) (void)hipEventDestroy(e);
-    if (ev_a) (void)hipEventDestroy(ev_a);
-    if (ev_b) (void)hipEventDestroy(ev_b);
-    if (st_b) (void)hipStreamSynchronize(st_b);
+    for (hipEvent_t e : {ev_a, ev_b, ev_s0, ev_s1})
+      if (e) (void)hipEventDestroy(e);
     for (int q = 0; q < 2; ++q) {
       if (ev_int[q]) (void)hipEventDestroy(ev_int[q]);
       if (ev_bnd[q]) (void)hipEventDestroy(ev_bnd[q]);
@@ -319,6 +329,9 @@ class Solver {
     if (ev_sync) (void)hipEventDestroy(ev_sync);
     if (st_b) (void)hipStreamDestroy(st_b);
     if (st) (void)hipStreamDestroy(st);
+    ev_poll[0] = ev_poll[1] = ev_a = ev_b = ev_s0 = ev_s1 = ev_sync = nullptr;
+    ev_int[0] = ev_int[1] = ev_bnd[0] = ev_bnd[1] = nullptr;
+    st = st_b = nullptr;
   }
 
   void validate() const {
@@ -333,8 +346,6 @@ class Solver {
     if (P.sweeps_per_launch == 3 && P.case_id != CFD_CAVITY)
       throw Error(CFD_E_ARG, "three sweeps per launch are implemented for the cavity only");
     if (P.ordering != CFD_ORDER_RB && P.ordering != CFD_ORDER_LEX) throw Error(CFD_E_ARG, "unknown ordering");
-    if (P.ordering == CFD_ORDER_LEX && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
-      throw Error(CFD_E_ARG, "lexicographic ordering supports nx + ny < 12000");
     if (P.ordering == CFD_ORDER_LEX && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
       throw Error(CFD_E_ARG, "lexicographic ordering supports nx + ny < 12000");
     if (P.case_id == CFD_BACKSTEP && (P.step_i <= 0 || P.step_i >= P.nx))
@@ -526,16 +537,6 @@ class Solver {
       if (n >= 2) {
         const PairPlan pl = multi_plan(g.wj0, g.wj1 + 1, 0, 0, resident_pair_waves / (int)S.size(), n);
         launch_multi<CASE>(n, pl, g, pin[q], pout[q], S[q].b[B_F], ctl, k, ka, kb, st, replay);
-      } else if (kernel_variant == 1) {  // legacy variants (one sweep per launch only): test k-1 themselves
-        const dim3 grid((P.nx + 2 + PBX - 1) / PBX, (rows + PBY - 1) / PBY);
-        poisson_rbsor_kernel<CASE, PBX, PBY><<<grid, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k);
-      } else if (kernel_variant == 2) {
-        constexpr int TW = 256 - 8;
-        // one resident round: split each column tile's rows evenly over the
-        // blocks the device holds at once (no tail of a second, partial round)
-        wave_bands(rows, TW, resident_blocks, ctiles, th, nbands);
-        poisson_march_kernel<CASE><<<ctiles * nbands, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k, th,
-                                                                    ctiles, nbands, march_flags);
       } else {
         wave_bands(rows, 128 - 8, resident_waves, ctiles, th, nbands);
         const int nblk = (ctiles * nbands + 3) / 4;
@@ -555,13 +556,26 @@ class Solver {
   }
 
   // all-reduce (max) of the residual slots of iterations k .. k+n-1 that are tested
+  // (slots adjacent in the ring go in one call: one RCCL latency per launch)
   void allreduce_slots(int k, int n, hipStream_t xs) {
+    constexpr size_t SLOT = (size_t)RES_SHARDS * SHARD_STRIDE;
+    int run0 = -1, runn = 0;  // ring slots [run0, run0 + runn) pending
+    auto flush = [&] {
+      if (runn > 0) comm_allreduce_max(comm, ring + (size_t)run0 * SLOT, SLOT * runn, xs);
+      runn = 0;
+    };
     for (int kk = k; kk < k + n && kk <= P.max_iters; ++kk) {
-      if (kk % P.check_every == 0 || kk == P.max_iters) {
-        double* slot = ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-        comm_allreduce_max(comm, slot, RES_SHARDS * SHARD_STRIDE, xs);
+      if (!(kk % P.check_every == 0 || kk == P.max_iters)) continue;
+      const int sl = kk & (RING - 1);
+      if (runn > 0 && sl == run0 + runn) {
+        ++runn;
+      } else {
+        flush();
+        run0 = sl;
+        runn = 1;
       }
     }
+    flush();
   }
 
   // Launch m (n >= 2 sweeps) on a rank with halo overlap. st_b: exchange of
@@ -617,7 +631,7 @@ class Solver {
   void poisson_launch(int m, int k, int n, int base, int ka, int kb, bool replay) {
     const int bin = pbuf((base + m) % nbufs());
     const int bout = pbuf((base + m + 1) % nbufs());
-    if (overlap && n >= 2 && !replay && kernel_variant == 0) {
+    if (overlap && n >= 2 && !replay) {
       if (P.case_id == CFD_CAVITY) multi_overlapped<CAVITY>(m, k, n, ka, kb, bin, bout);
       else if (P.case_id == CFD_CHANNEL) multi_overlapped<CHANNEL>(m, k, n, ka, kb, bin, bout);
       else multi_overlapped<BACKSTEP>(m, k, n, ka, kb, bin, bout);
@@ -834,7 +848,19 @@ class Solver {
   }
 
   // run() loop body: cavity-01.cpp:387-390; channel-01.cpp:368-375.
+  // adds the last timed step's device time to T.step_ms (waits for it)
+  void flush_step_time() {
+    if (!step_timed) return;
+    HIPC(hipEventSynchronize(ev_s1));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ev_s0, ev_s1));
+    T.step_ms += ms;
+    step_timed = false;
+  }
+
   void step(cfd_step_info* out) {
+    flush_step_time();
+    HIPC(hipEventRecord(ev_s0, st));
     if (P.case_id == CFD_CAVITY) {
       apply_bc(false);
       compute_tentative();
@@ -850,6 +876,8 @@ class Solver {
       correct();
       apply_bc(false);
     }
+    HIPC(hipEventRecord(ev_s1, st));
+    step_timed = true;
     T.steps += 1;
   }
 
@@ -1016,7 +1044,14 @@ cfd_solver* cfd_create_rank(const cfd_params* p, int device, int row_begin, int 
   guard([&] {
     if (!p) throw Error(CFD_E_ARG, "null params");
     if (row_begin < 1 || row_end > p->ny || row_end - row_begin + 1 < cfd::HALO)
-      throw Error(CFD_E_ARG, "rank rows must lie in [1, ny] and span at least 4 rows");
+      throw Error(CFD_E_ARG, "rank rows must lie in [1, ny] and span at least 8 rows (the SOR halo depth)");
+    // the halo exchange talks to ranks rank-1 (rows below) and rank+1 (rows
+    // above): ranks must own consecutive row blocks in rank order
+    if (auto* cm = static_cast<cfd::Comm*>(comm)) {
+      if ((cm->rank == 0) != (row_begin == 1) || (cm->rank == cm->nranks - 1) != (row_end == p->ny))
+        throw Error(CFD_E_ARG, "rank rows do not match the communicator rank (rank 0 must own row 1, the last "
+                               "rank row ny, ranks in row order)");
+    }
     out = new cfd_solver{new Solver(*p, device, {{row_begin, row_end}}, static_cast<cfd::Comm*>(comm))};
   });
   return out;
@@ -1098,10 +1133,18 @@ int cfd_write_pvd(const char* filename, const char* const* files, const double* 
 int cfd_get_timing(cfd_solver* s, cfd_timing* out) {
   return guard([&] {
     if (!out) throw Error(CFD_E_ARG, "null output");
-    *out = S_(s)->T;
+    Solver* v = S_(s);
+    v->flush_step_time();
+    *out = v->T;
   });
 }
-int cfd_reset_timing(cfd_solver* s) { return guard([&] { S_(s)->T = cfd_timing{}; }); }
+int cfd_reset_timing(cfd_solver* s) {
+  return guard([&] {
+    Solver* v = S_(s);
+    v->flush_step_time();
+    v->T = cfd_timing{};
+  });
+}
 int cfd_synchronize(cfd_solver* s) { return guard([&] { HIPC(hipStreamSynchronize(S_(s)->st)); }); }
 
 int cfd_owned_rows(const cfd_solver* s, int* first, int* last) {
@@ -1129,6 +1172,13 @@ void* cfd_comm_init(const unsigned char* id, int nranks, int rank, int device) {
 }
 
 int cfd_comm_destroy(void* comm) { return guard([&] { cfd::comm_destroy(static_cast<cfd::Comm*>(comm)); }); }
+
+int cfd_comm_info(void* comm, int* nranks, int* rank, int* transport) {
+  return guard([&] {
+    if (!nranks || !rank || !transport) throw Error(CFD_E_ARG, "null output");
+    cfd::comm_info(static_cast<cfd::Comm*>(comm), nranks, rank, transport);
+  });
+}
 
 void* cfd_comm_loopback_hub(int nranks) {
   void* out = nullptr;

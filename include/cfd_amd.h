@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 3
+#define CFD_AMD_ABI_VERSION 4
 
 /* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
  * tree (only figures): it is the cavity's projection step with a resting lid
@@ -179,6 +179,9 @@ int cfd_synchronize(cfd_solver* s);
 int cfd_comm_unique_id(unsigned char* id_out);
 void* cfd_comm_init(const unsigned char* id, int nranks, int rank, int device);
 int cfd_comm_destroy(void* comm);
+/* What the transport itself reports: for RCCL, ncclCommCount / ncclCommUserRank
+ * (so a host can show that RCCL saw every rank); transport 0 = RCCL, 1 = loopback. */
+int cfd_comm_info(void* comm, int* nranks, int* rank, int* transport);
 
 /* In-process transport with the same semantics, for ranks that share one
  * device and run in separate host threads of one process (RCCL refuses two

@@ -1,0 +1,76 @@
+"""Child process of tests/test_gpu_rccl.py (two GPUs): spawns two ranks, one
+per device, each as bench.py at N=2 (torch first, gloo group, RCCL
+communicator through the library), runs the rank-path solver over real RCCL
+(grouped ncclSend/ncclRecv halos, overlapped lagged residual all-reduce) and
+compares its rows with a single-domain solver on the same device. Prints one
+JSON line for the test."""
+import json
+import os
+import sys
+
+import torch  # noqa: F401  (first: the library binds to PyTorch's HIP runtime)
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "computational-fluid-dynamics_amd"))
+import numpy as np  # noqa: E402
+
+
+def rank_main(rank, world, case, ny, steps, q):
+    import cfd_amd as C
+    from cfd_amd import _lib
+    from cfd_amd.dist import comm_info, init_comm, strip_rows
+
+    torch.cuda.set_device(rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = init_comm(dist, rank, world, rank)
+    info = comm_info(comm)
+    cp = C.make_params(case, nx=96, ny=ny)
+    s = C.solver_for(cp, device=rank, rank_rows=strip_rows(rank, world, ny), comm=comm, check_every=1)
+    if case == "cavity":
+        s.applyBoundaryConditions()
+    its = [s.step() for _ in range(steps)]
+    rows = s.owned_rows()
+    fields = {n: s.field(n) for n in ("u", "v", "p")}
+    overlapped = s.timing().poisson_overlapped > 0
+    s.close()
+    dist.barrier()
+    _lib.lib().cfd_comm_destroy(comm)
+    r = C.solver_for(cp, device=rank)
+    if case == "cavity":
+        r.applyBoundaryConditions()
+    its_ref = [r.step() for _ in range(steps)]
+    j0, j1 = rows
+    first = 0 if j0 == 1 else j0
+    ok = True
+    for n, a in fields.items():
+        ref = r.field(n)
+        last = min(j1 + 1 if j1 == ny else j1, ref.shape[0] - 1)
+        b = ref[first:last + 1]
+        if case == "cavity":
+            ok &= bool(np.array_equal(a.view(np.int64), b.view(np.int64)))
+        else:
+            ok &= bool(np.abs(a - b).max() <= 1e-9 * max(np.abs(b).max(), 1.0))
+    r.close()
+    dist.destroy_process_group()
+    q.put((rank, info, [int(i) for i, _ in its] == [int(i) for i, _ in its_ref], ok, overlapped))
+
+
+def main() -> int:
+    case, ny, steps = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=rank_main, args=(r, 2, case, ny, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=150) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+    print(json.dumps({"comm": [o[1] for o in out], "its_equal": all(o[2] for o in out),
+                      "fields_ok": all(o[3] for o in out), "overlapped": [o[4] for o in out]}), flush=True)
+    return 0 if all(p.exitcode == 0 for p in procs) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -125,9 +125,11 @@ def _worker(rank, world, port, q, nx, ny, iters, spl):
 
 
 @pytest.mark.parametrize("spl", [2, 3])
-@pytest.mark.parametrize("world", [2])
-def test_two_rank_strips_equal_single_domain(world, spl):
-    nx, ny, iters = 24, 20, 15
+@pytest.mark.parametrize("world,nx,ny", [(2, 24, 20), (2, 40, 1024)])
+def test_two_rank_strips_equal_single_domain(world, nx, ny, spl):
+    """(2, 40, 1024): 512 rows per rank, the strip height of the strong-scaling
+    bench (4096² over 8 GPUs)."""
+    iters = 15
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()

@@ -1,0 +1,133 @@
+"""BASELINE.json configs[0], [1], [3], [4] at their stated sizes, on the GPU,
+against the CPU oracle.
+
+* configs[0] cavity Re=100, 128², dt=1e-3 (README "Run It": --Re 100 --Nx 128
+  --Ny 128 --dt 1e-3): whole timesteps bit-exact against the red-black oracle
+  (iteration counts included) and, since this solve converges, centerline u/v
+  within 1e-6 relative L2 of the reference's own lexicographic ordering.
+* configs[1] cavity Re=1000, 1024²: whole timesteps bit-exact against the
+  red-black oracle with the sweeps capped (CPU time), and a full uncapped step
+  whose reported residual is the true residual of the returned field and
+  meets the reference's stop rule.
+* configs[3] backwards step Re=400, 8192x512 on 4 ranks (loopback transport,
+  the RCCL code path): every rank's rows against the red-black oracle, not
+  only against one GPU domain.
+* configs[4] Rayleigh-Benard Ra=1e6 Pr=0.71, 8192x2048 (parity unpinned: no
+  reference solver): a whole step bit-exact against the oracle's restatement,
+  and 4 strips == one domain, at the full size.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import cfd_amd as C  # noqa: E402
+import oracle as O  # noqa: E402
+from test_gpu_fullsize import cavity_residual  # noqa: E402
+from test_gpu_parity import assert_bits, centerlines, ofield, rel_l2  # noqa: E402
+from test_gpu_ranks import run_ranks  # noqa: E402
+
+
+def test_config0_cavity_re100_128_bitexact_and_reference_order():
+    cp = C.make_params("cavity", re=100.0, nx=128, ny=128, dt=1e-3)
+    assert cp.total_steps == 20000 and cp.nu == pytest.approx(0.01)
+    g = C.CavitySolver(cp)
+    orb = O.Oracle(cp, ordering=O.RB)
+    olex = O.Oracle(cp, ordering=O.LEX)
+    g.applyBoundaryConditions()
+    for k in range(40):
+        ig, rg = g.step()
+        ir, rr = orb.step()
+        il, _ = olex.step()
+        assert (ig, rg) == (ir, rr), k
+        assert ig < cp.max_iters and il < cp.max_iters  # both orderings converge to the tolerance
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(orb, name, cp), f"config0 {name}")
+    g.statistics()
+    olex.centers()
+    ug, vg = centerlines(g.field("uc"), g.field("vc"), cp)
+    ul, vl = centerlines(olex.field("uc"), olex.field("vc"), cp)
+    scale = np.linalg.norm(ul)
+    du, dv = np.linalg.norm(ug - ul) / scale, np.linalg.norm(vg - vl) / max(scale, np.linalg.norm(vl))
+    print(f"config0 centerline rel-L2 vs reference order: u {du:.3e} v {dv:.3e}")
+    assert du <= 1e-6 and dv <= 1e-6
+
+
+def test_config1_cavity_1024_steps_bitexact_capped():
+    cp = C.make_params("cavity", re=1000.0, nx=1024, ny=1024, max_iters=300)
+    g = C.CavitySolver(cp)
+    o = O.Oracle(cp, ordering=O.RB)
+    g.applyBoundaryConditions()
+    for k in range(2):
+        ig, rg = g.step()
+        io, ro = o.step()
+        assert (ig, rg) == (io, ro), k
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"config1 {name}")
+
+
+def test_config1_cavity_1024_full_step_meets_reference_stop_rule():
+    """Uncapped (cap 10000): the solve stops at the first sweep whose max-norm
+    residual is <= 1e-9 max|src| (cavity-01.cpp:632-635), and that residual is
+    the true residual of the field returned (recomputed here)."""
+    cp = C.make_params("cavity", re=1000.0, nx=1024, ny=1024)
+    g = C.CavitySolver(cp)
+    g.applyBoundaryConditions()
+    g.computeTentativeVelocities()
+    g.buildSourceTerm()
+    it, res = g.solverPressurePoisson()
+    f = g.field("src")
+    tol = cp.tol_factor * np.abs(f[1:-1, 1:-1]).max()
+    assert 1 < it < cp.max_iters
+    assert res <= tol
+    assert res == cavity_residual(g.field("p"), f, cp.dx)
+    # one sweep fewer does not meet it
+    cq = C.make_params("cavity", re=1000.0, nx=1024, ny=1024, max_iters=it - 1)
+    q = C.CavitySolver(cq)
+    q.applyBoundaryConditions()
+    q.computeTentativeVelocities()
+    q.buildSourceTerm()
+    it2, res2 = q.solverPressurePoisson()
+    assert it2 == it - 1 and res2 > tol
+
+
+def test_config3_backstep_8192x512_four_ranks_vs_oracle():
+    cp = C.make_params("backwards_step", re=400.0, nx=8192, ny=512, max_iters=40)
+    steps = 2
+    res = run_ranks(cp, 4, steps)
+    o = O.Oracle(cp, ordering=O.RB)
+    o.velocity_bc(False)
+    its = [o.step() for _ in range(steps)]
+    for r in res:
+        assert [i for i, _ in r["its"]] == [i for i, _ in its]
+        j0, j1 = r["rows"]
+        first = 0 if j0 == 1 else j0
+        for name in ("u", "v", "p"):
+            ref = ofield(o, name, cp)
+            last = min(j1 + 1 if j1 == cp.ny else j1, ref.shape[0] - 1)
+            # source mean: per-rank tree sums all-reduced vs one sequential sum
+            np.testing.assert_allclose(r[name], ref[first:last + 1], rtol=0,
+                                       atol=1e-10 * max(np.abs(ref).max(), 1.0), err_msg=f"{name} rows {j0}-{j1}")
+
+
+def test_config4_rayleigh_benard_8192x2048_step_vs_oracle():
+    cp = C.make_params("rayleigh_benard", ra=1e6, pr=0.71, nx=8192, ny=2048, max_iters=30)
+    g = C.RayleighBenardSolver(cp)
+    o = O.Oracle(cp, ordering=O.RB)
+    assert g.step() == o.step()
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"config4 {name}")
+    assert_bits(g.field("t")[1:-1, 1:-1], o.field("t")[1:-1, 1:-1], "config4 T")
+
+
+def test_config4_rayleigh_benard_8192x2048_strips_equal_single_domain():
+    cp = C.make_params("rayleigh_benard", ra=1e6, pr=0.71, nx=8192, ny=2048, max_iters=60)
+    a = C.RayleighBenardSolver(cp)
+    b = C.RayleighBenardSolver(cp, n_strips=4)
+    for _ in range(2):
+        assert a.step() == b.step()
+    for name in ("u", "v", "p", "t"):
+        assert_bits(b.field(name), a.field(name), f"config4 strips {name}")
+    assert rel_l2(b.field("t"), a.field("t")) == 0.0

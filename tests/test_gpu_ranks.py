@@ -91,8 +91,9 @@ def test_rank_path_equals_single_domain(case, world, steps):
 
 
 def test_rank_path_check_every_8():
-    """The multi-GPU default tests the residual every 8 sweeps: it may run up to 7
-    sweeps past the reference's stopping point, never fewer, and still converges."""
+    """check_every=8 (an option; every GPU count defaults to 1, the reference's
+    rule): the solve may run up to 7 sweeps past the reference's stopping
+    point, never fewer, and still converges."""
     cp = C.reference_defaults("cavity")
     res = run_ranks(cp, 2, 5, check_every=8)
     _, its = single(cp, 5)
