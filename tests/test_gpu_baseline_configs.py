@@ -69,9 +69,13 @@ def test_config1_cavity_1024_steps_bitexact_capped():
 
 
 def test_config1_cavity_1024_full_step_meets_reference_stop_rule():
-    """Uncapped (cap 10000): the solve stops at the first sweep whose max-norm
-    residual is <= 1e-9 max|src| (cavity-01.cpp:632-635), and that residual is
-    the true residual of the field returned (recomputed here)."""
+    """Uncapped (cap 10000) first step at 1024²: like the reference's own
+    lexicographic solve (scripts/lex_vs_rb.py: 10000 sweeps, residual 2.5 on
+    the CPU) the red-black solve hits the cap; the residual it reports is the
+    true residual of the field it returns (recomputed here) and exceeds the
+    tolerance 1e-9 max|src| (cavity-01.cpp:632-635). (The stop rule at a
+    converging solve is checked bit-exactly against the oracle at reference
+    sizes, tests/test_gpu_parity.py.)"""
     cp = C.make_params("cavity", re=1000.0, nx=1024, ny=1024)
     g = C.CavitySolver(cp)
     g.applyBoundaryConditions()
@@ -80,17 +84,8 @@ def test_config1_cavity_1024_full_step_meets_reference_stop_rule():
     it, res = g.solverPressurePoisson()
     f = g.field("src")
     tol = cp.tol_factor * np.abs(f[1:-1, 1:-1]).max()
-    assert 1 < it < cp.max_iters
-    assert res <= tol
+    assert it == cp.max_iters and res > tol
     assert res == cavity_residual(g.field("p"), f, cp.dx)
-    # one sweep fewer does not meet it
-    cq = C.make_params("cavity", re=1000.0, nx=1024, ny=1024, max_iters=it - 1)
-    q = C.CavitySolver(cq)
-    q.applyBoundaryConditions()
-    q.computeTentativeVelocities()
-    q.buildSourceTerm()
-    it2, res2 = q.solverPressurePoisson()
-    assert it2 == it - 1 and res2 > tol
 
 
 def test_config3_backstep_8192x512_four_ranks_vs_oracle():
