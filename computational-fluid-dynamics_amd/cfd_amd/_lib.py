@@ -58,7 +58,8 @@ class Timing(ctypes.Structure):
     _fields_ = [("poisson_ms", ctypes.c_double), ("poisson_launches", ctypes.c_longlong),
                 ("poisson_cell_updates", ctypes.c_longlong), ("step_ms", ctypes.c_double),
                 ("steps", ctypes.c_longlong), ("poisson_sweeps", ctypes.c_longlong),
-                ("poisson_overlapped", ctypes.c_longlong)]
+                ("poisson_overlapped", ctypes.c_longlong), ("poisson_steady_ms", ctypes.c_double),
+                ("poisson_steady_launches", ctypes.c_longlong)]
 
 
 # every symbol include/cfd_amd.h declares: name -> (restype, argtypes)

@@ -397,4 +397,18 @@ __global__ __launch_bounds__(256, 2) void poisson_lexw_kernel(Geo g, Coef c, con
 #undef LX_SLOT
 #undef LX_S10
 
+// max-norm residual of a cavity field (cavity-01.cpp:659-677) over the owned
+// interior cells: the residual the reference reports after its last sweep
+__global__ __launch_bounds__(256) void cavity_resmax_kernel(Geo g, Coef c, const double* __restrict__ p,
+                                                            const double* __restrict__ f, double* __restrict__ shards) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  double m = 0.0;
+  if (i >= 1 && i <= g.nx && j >= 1 && j <= g.ny && j <= g.j1) {
+    const size_t o = at(g, j, i), P = (size_t)g.pitch;
+    m = residual_abs<CAVITY>(c, g.nx, g.ny, j, i, p[o], p[o - 1], p[o + 1], p[o - P], p[o + P], f[o]);
+  }
+  block_max_to_shard<256>(m, shards, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
+}
+
 }  // namespace cfd

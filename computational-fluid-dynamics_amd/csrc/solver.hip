@@ -17,6 +17,7 @@
 
 #include "internal.hpp"
 #include "kernels.hpp"
+#include "lexw.hpp"
 
 namespace cfd {
 
@@ -143,6 +144,17 @@ class Solver {
   int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order
   int march_min_th = MARCH_MIN_TH;
 
+  // The reference's lexicographic order at any size (lexw.hpp): per-slot
+  // exceedance bitset, final-residual shards, events around the steady-state
+  // launches (no ramp), resident waves of the lexw kernel.
+  unsigned long long* lexbits = nullptr;
+  size_t lexbits_words = 0;
+  double* resmax = nullptr;
+  hipEvent_t ev_f0 = nullptr, ev_f1 = nullptr;
+  int resident_lexw_waves = 2048;
+  bool use_lexw() const { return P.ordering == CFD_ORDER_LEX && P.case_id == CFD_CAVITY; }
+  int lexw_ns() const { return P.sweeps_per_launch >= 1 ? P.sweeps_per_launch : 2; }
+
   // Rayleigh-Benard: the cavity's projection (P.case_id is set to CFD_CAVITY,
   // u_ref 0 = lid at rest) plus the temperature stage on tcur/tnext.
   bool thermal = false;
@@ -189,6 +201,13 @@ class Solver {
         HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pps, poisson_multi_kernel<BACKSTEP, 2>, 256, 0));
       pps = std::max(1, std::min(pps, 4));
       if (const char* e = std::getenv("CFD_PAIR_WPS")) pps = std::max(1, std::atoi(e));
+      if (use_lexw()) {
+        int lps = 0;
+        if (lexw_ns() == 1) HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<1>, 256, 0));
+        else if (lexw_ns() == 2) HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<2>, 256, 0));
+        else HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<3>, 256, 0));
+        resident_lexw_waves = std::max(1, std::min(lps, 4)) * 4 * prop.multiProcessorCount;
+      }
       if (const char* e = std::getenv("CFD_PAIR_EDGE_PCT")) pair_edge_pct = std::max(10, std::min(100, std::atoi(e)));
       resident_pair_waves = pps * 4 * prop.multiProcessorCount;
     }
@@ -226,6 +245,7 @@ class Solver {
     HIPC(hipMalloc(&total, 4 * sizeof(double)));
     HIPC(hipMalloc(&partials, std::max<size_t>(npart, 1) * sizeof(double)));
     HIPC(hipMalloc(&stop, 2 * sizeof(int)));
+    HIPC(hipMalloc(&resmax, RES_SHARDS * SHARD_STRIDE * sizeof(double)));
     HIPC(hipMemsetAsync(ring, 0, ringn * sizeof(double), st));
     HIPC(hipMemsetAsync(tolv, 0, 2 * sizeof(double), st));
     HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
@@ -236,6 +256,8 @@ class Solver {
     HIPC(hipEventCreate(&ev_b));
     HIPC(hipEventCreate(&ev_s0));
     HIPC(hipEventCreate(&ev_s1));
+    HIPC(hipEventCreate(&ev_f0));
+    HIPC(hipEventCreate(&ev_f1));
     if (comm && comm->nranks > 1 && S.size() == 1) {
       const Geo& g0 = S[0].g;
       const char* e = std::getenv("CFD_OVERLAP");
@@ -309,9 +331,12 @@ class Solver {
       for (auto* p : s.b)
         if (p) (void)hipFree(p);
     S.clear();
-    for (double* p : {ring, srcmax, divmax, tolv, total, partials})
+    for (double* p : {ring, srcmax, divmax, tolv, total, partials, resmax})
       if (p) (void)hipFree(p);
-    ring = srcmax = divmax = tolv = total = partials = nullptr;
+    ring = srcmax = divmax = tolv = total = partials = resmax = nullptr;
+    if (lexbits) (void)hipFree(lexbits);
+    lexbits = nullptr;
+    lexbits_words = 0;
     if (stop) (void)hipFree(stop);
     stop = nullptr;
     if (h_stat) (void)hipHostFree(h_stat);
@@ -320,7 +345,7 @@ class Solver {
     h_shard = nullptr;
     for (auto& e : ev_poll)
       if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {ev_a, ev_b, ev_s0, ev_s1})
+    for (hipEvent_t e : {ev_a, ev_b, ev_s0, ev_s1, ev_f0, ev_f1})
       if (e) (void)hipEventDestroy(e);
     for (int q = 0; q < 2; ++q) {
       if (ev_int[q]) (void)hipEventDestroy(ev_int[q]);
@@ -329,7 +354,7 @@ class Solver {
     if (ev_sync) (void)hipEventDestroy(ev_sync);
     if (st_b) (void)hipStreamDestroy(st_b);
     if (st) (void)hipStreamDestroy(st);
-    ev_poll[0] = ev_poll[1] = ev_a = ev_b = ev_s0 = ev_s1 = ev_sync = nullptr;
+    ev_poll[0] = ev_poll[1] = ev_a = ev_b = ev_s0 = ev_s1 = ev_f0 = ev_f1 = ev_sync = nullptr;
     ev_int[0] = ev_int[1] = ev_bnd[0] = ev_bnd[1] = nullptr;
     st = st_b = nullptr;
   }
@@ -346,8 +371,10 @@ class Solver {
     if (P.sweeps_per_launch == 3 && P.case_id != CFD_CAVITY)
       throw Error(CFD_E_ARG, "three sweeps per launch are implemented for the cavity only");
     if (P.ordering != CFD_ORDER_RB && P.ordering != CFD_ORDER_LEX) throw Error(CFD_E_ARG, "unknown ordering");
-    if (P.ordering == CFD_ORDER_LEX && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
-      throw Error(CFD_E_ARG, "lexicographic ordering supports nx + ny < 12000");
+    // (the cavity's lexicographic solve runs on the multi-block wavefront kernel
+    // at any size; the open cases on the one-workgroup kernel)
+    if (P.ordering == CFD_ORDER_LEX && P.case_id != CFD_CAVITY && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
+      throw Error(CFD_E_ARG, "lexicographic ordering of the open cases supports nx + ny < 12000");
     if (P.case_id == CFD_BACKSTEP && (P.step_i <= 0 || P.step_i >= P.nx))
       throw Error(CFD_E_ARG, "Step location is outside computational domain!");
     if (P.case_id == CFD_BACKSTEP && (P.inlet_jmax < 1 || P.inlet_jmax > P.ny))
@@ -484,7 +511,7 @@ class Solver {
   // rows, marched in groups of 10 over th + march_extra rows, so th + extra is
   // a multiple of 10. The two boundary column tiles march slower (masks):
   // shorter bands, pair_edge_pct % of the interior march.
-  PairPlan multi_plan(int lo0, int hi0, int lo1, int hi1, int waves, int n) const {
+  PairPlan multi_plan(int lo0, int hi0, int lo1, int hi1, int waves, int n, int max_th = 1 << 30) const {
     PairPlan pl{};
     pl.ctiles = (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC;
     pl.lo0 = lo0; pl.hi0 = hi0; pl.lo1 = lo1; pl.hi1 = hi1;
@@ -494,8 +521,18 @@ class Solver {
     const int ex = march_extra(n);
     auto nbands = [](int lo, int hi, int t) { return hi > lo ? (hi - lo + t - 1) / t : 0; };
     int nb = std::max(1, std::min(waves / std::max(1, pl.ctiles), (rows + march_min_th - 1) / march_min_th));
+    nb = std::max(nb, (rows + max_th - 1) / max_th);
     for (;; --nb) {  // most interior bands whose tiles (boundary tiles included) fit one round
       pl.th = std::max(1, std::min(rmax, ((rows + nb - 1) / nb + ex + 9) / 10 * 10 - ex));
+      if (pl.th > max_th) {  // (lexw: one wave marches at most max_th rows)
+        pl.th = max_th;
+        pl.the = std::max(8, std::min(rmax, (pl.th + ex) * pair_edge_pct / 100 - ex));
+        pl.nb0 = nbands(lo0, hi0, pl.th);
+        pl.nb1 = nbands(lo1, hi1, pl.th);
+        pl.nbe0 = nbands(lo0, hi0, pl.the);
+        pl.nbe1 = nbands(lo1, hi1, pl.the);
+        break;
+      }
       pl.the = std::max(8, std::min(rmax, (pl.th + ex) * pair_edge_pct / 100 - ex));
       pl.nb0 = nbands(lo0, hi0, pl.th);
       pl.nb1 = nbands(lo1, hi1, pl.th);
@@ -696,7 +733,190 @@ class Solver {
     }
   }
 
+  // ---- lexicographic order, multi-block (lexw.hpp) ----
+  static int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+  // iterations whose residual every cell has contributed after launch m (H0 = 2 + 2NS m)
+  int lexw_done(int m, int ns) const { return m < 0 ? 0 : floordiv(2 + 2 * ns * m + 2 * ns - 2 - P.nx - P.ny, 2) + 1; }
+
+  void launch_lexw(int ns, const PairPlan& pl, const Geo& g, const double* pin, double* pout, const double* f,
+                   const LexCtl& L, int H0, int K, int ka, int kb, bool replay) {
+    const int fl = replay ? 4 : 0;
+    const int ne = pl.ctiles >= 2 ? 2 : 1;
+    const int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
+    if (ntiles == 0) return;
+    const dim3 grid((ntiles + 3) / 4);
+    if (ns == 1) poisson_lexw_kernel<1><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl);
+    else if (ns == 2) poisson_lexw_kernel<2><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl);
+    else poisson_lexw_kernel<3><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl);
+  }
+
+  // K lexicographic iterations of every cell as launches m = 0.. (half-sweeps
+  // H0 = 2 + 2NS m ..), starting from buffer `base`; with tests, launch m first
+  // tests the iterations completed by launch m-1. Returns the launches run
+  // (the result is in pbuf((base + launches) % 2)); *kstop = the iteration the
+  // solve stopped at, or -1.
+  int run_lexw(int base, int K, bool tests, int* kstop, bool time_steady) {
+    const int ns = lexw_ns();
+    const int Hlast = P.nx + P.ny + 2 * (K - 1);
+    const int nl = (Hlast - 2) / (2 * ns) + 1;  // last launch covers Hlast
+    const int kmax = P.max_iters + (P.nx + P.ny) / 2 + 64;
+    LexCtl L{lexbits, (int)(lexbits_words / LEXW_SHARDS), kmax, tolv, stop};
+    std::vector<PairPlan> plans(S.size());
+    for (size_t q = 0; q < S.size(); ++q)
+      plans[q] = multi_plan(S[q].g.wj0, S[q].g.wj1 + 1, 0, 0, resident_lexw_waves / (int)S.size(), ns, 200);
+    // steady launches: every cell active in every half-sweep (H0 >= nx+ny, H0+2NS-1 <= 2K)
+    const int ms0 = (P.nx + P.ny - 2 + 2 * ns - 1) / (2 * ns), ms1 = (2 * K - 2 * ns + 1 - 2) / (2 * ns);
+    const bool steady = time_steady && ms1 >= ms0 && ms0 >= 0;
+    const int chunk = P.chunk > 0 ? P.chunk : 32;
+    int tested = tests ? -1 : K;  // highest iteration tested
+    bool stopped = false;
+    int m = 0, c = 0;
+    *kstop = -1;
+    while (m < nl && !stopped) {
+      for (int jj = 0; jj < chunk && m < nl; ++jj, ++m) {
+        int ka = 1, kb = 0;
+        if (tests) {
+          if (m == 0) {
+            ka = kb = 0;
+          } else {
+            ka = tested + 1;
+            kb = std::min(lexw_done(m - 1, ns), K - 1);
+          }
+          if (ka <= kb) tested = kb;
+        }
+        const int bin = pbuf((base + m) % 2), bout = pbuf((base + m + 1) % 2);
+        if (multi()) exchange(bin, HALO);
+        if (steady && m == ms0) HIPC(hipEventRecord(ev_f0, st));
+        for (size_t q = 0; q < S.size(); ++q)
+          launch_lexw(ns, plans[q], S[q].g, S[q].b[bin], S[q].b[bout], S[q].b[B_F], L, 2 + 2 * ns * m, K, ka, kb,
+                      !tests);
+        check_launch("poisson_lexw");
+        if (steady && m == ms1) HIPC(hipEventRecord(ev_f1, st));
+      }
+      if (tests) {
+        HIPC(hipMemcpyAsync(h_stat + 2 * (c & 1), stop, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+        HIPC(hipEventRecord(ev_poll[c & 1], st));
+        if (c > 0) {
+          HIPC(hipEventSynchronize(ev_poll[(c - 1) & 1]));
+          if (h_stat[2 * ((c - 1) & 1)] != 0) stopped = true;
+        }
+        ++c;
+      }
+    }
+    if (tests) {
+      HIPC(hipStreamSynchronize(st));
+      HIPC(hipMemcpy(h_stat, stop, 2 * sizeof(int), hipMemcpyDeviceToHost));
+      if (h_stat[0]) {
+        *kstop = h_stat[1];
+      } else if (tested < K - 1) {  // iterations completed by the last launches: tested here, in order
+        std::vector<unsigned long long> hb(lexbits_words);
+        HIPC(hipMemcpy(hb.data(), lexbits, lexbits_words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        const size_t wps = lexbits_words / LEXW_SHARDS;
+        for (int k = std::max(tested + 1, 1); k <= K - 1; ++k) {
+          const int qb = kmax - k;
+          unsigned long long w = 0;
+          for (int sh = 0; sh < LEXW_SHARDS; ++sh) w |= hb[(size_t)sh * wps + (qb >> 6)];
+          if (!((w >> (qb & 63)) & 1ull)) {
+            *kstop = k;
+            break;
+          }
+        }
+      }
+    }
+    if (steady && m > ms1) {  // (both events recorded: the solve did not stop before the last steady launch)
+      HIPC(hipEventSynchronize(ev_f1));
+      float ms = 0.f;
+      HIPC(hipEventElapsedTime(&ms, ev_f0, ev_f1));
+      T.poisson_steady_ms += ms;
+      T.poisson_steady_launches += ms1 - ms0 + 1;
+    }
+    return m;
+  }
+
+  // solverPressurePoisson in the reference's own sweep order, any grid size.
+  void solve_lexw(cfd_step_info* out) {
+    if (comm) throw Error(CFD_E_STATE, "lexicographic ordering on ranks is not implemented (use strips on one device)");
+    const int ns = lexw_ns();
+    const int K = P.max_iters;
+    const int base = pcur & 1;
+    // cavity-01.cpp:610-611: each solve starts from a zero field (both buffers:
+    // cells not yet started are read from either)
+    for (auto& s : S)
+      for (int b : {0, 1}) HIPC(hipMemsetAsync(s.b[pbuf(b)], 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
+    solve_tolerance();
+    if (multi()) exchange(B_F, HALO - 1);
+    const int kmax = K + (P.nx + P.ny) / 2 + 64;
+    const size_t words = (size_t)LEXW_SHARDS * (kmax / 64 + 2);
+    if (lexbits_words < words) {
+      if (lexbits) HIPC(hipFree(lexbits));
+      lexbits = nullptr;
+      HIPC(hipMalloc(&lexbits, words * sizeof(unsigned long long)));
+      lexbits_words = words;
+    }
+    HIPC(hipMemsetAsync(lexbits, 0, lexbits_words * sizeof(unsigned long long), st));
+    HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
+    HIPC(hipEventRecord(ev_a, st));
+    int iters = K, kstop = -1, launched = 0, fin = base;
+    if (K > 0) {
+      launched = run_lexw(base, K, true, &kstop, true);
+      fin = (base + launched) % 2;
+      T.poisson_launches += launched;
+      T.poisson_sweeps += (long long)launched * ns;
+    } else {
+      kstop = 0;
+    }
+    if (kstop >= 0) {  // stopped at iteration kstop < K: every cell redoes exactly kstop iterations
+      iters = kstop;
+      for (auto& s : S)
+        for (int b : {0, 1}) HIPC(hipMemsetAsync(s.b[pbuf(b)], 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
+      fin = base;
+      if (kstop > 0) {
+        int dummy;
+        const int n2 = run_lexw(base, kstop, false, &dummy, false);
+        fin = (base + n2) % 2;
+        T.poisson_launches += n2;
+        T.poisson_sweeps += (long long)n2 * ns;
+      }
+    }
+    HIPC(hipEventRecord(ev_b, st));
+    // the reported residual: max-norm of the final field (cavity-01.cpp:659-677)
+    double res;
+    if (iters == 0) {
+      double t2[2];
+      HIPC(hipMemcpyAsync(t2, tolv, sizeof t2, hipMemcpyDeviceToHost, st));
+      HIPC(hipStreamSynchronize(st));
+      res = t2[1];
+    } else {
+      const int bp = pbuf(fin);
+      if (multi()) exchange(bp, 1);
+      HIPC(hipMemsetAsync(resmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
+      for (auto& s : S) {
+        cavity_resmax_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_F], resmax);
+        check_launch("cavity_resmax");
+      }
+      HIPC(hipMemcpyAsync(h_shard, resmax, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPC(hipStreamSynchronize(st));
+      res = 0.0;
+      for (int q = 0; q < RES_SHARDS; ++q) res = std::max(res, h_shard[q * SHARD_STRIDE]);
+    }
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
+    T.poisson_ms += ms;
+    long long owned = 0;
+    for (auto& s : S) owned += (long long)(s.g.j1 - s.g.j0 + 1) * P.nx;
+    T.poisson_cell_updates += owned * iters;
+    pcur = fin;
+    if (out) {
+      out->sor_iterations = iters;
+      out->residual = res;
+    }
+  }
+
   void solve(cfd_step_info* out) {
+    if (use_lexw()) {
+      solve_lexw(out);
+      return;
+    }
     if (P.ordering == CFD_ORDER_LEX) {
       solve_lex(out);
       return;

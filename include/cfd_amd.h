@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 4
+#define CFD_AMD_ABI_VERSION 5
 
 /* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
  * tree (only figures): it is the cavity's projection step with a resting lid
@@ -68,10 +68,12 @@ typedef struct cfd_params {
   int step_i, inlet_jmax;  /* derived step indices (backwards_step-01.cpp:386, 493) */
   int check_every;      /* residual test every N SOR iterations (1 = reference) */
   int chunk;            /* SOR launches enqueued between host polls (0 = auto) */
-  int ordering;         /* CFD_ORDER_RB (default, multi-block, strips/ranks) or CFD_ORDER_LEX
-                           (the reference's sweep order, bit-identical; one device, one strip) */
-  int sweeps_per_launch; /* red-black SOR iterations fused into one kernel launch: 0 = auto (3 for
-                           the cavity, 2 otherwise), 1, 2 or 3 (cavity); bit-identical either way */
+  int ordering;         /* CFD_ORDER_RB (red-black, strips/ranks) or CFD_ORDER_LEX (the reference's
+                           sweep order, bit-identical: cavity / Rayleigh-Benard at any size and in
+                           strips on one device; channel / step on one workgroup, nx+ny < 12000) */
+  int sweeps_per_launch; /* SOR iterations fused into one kernel launch: 0 = auto (red-black: 3 for
+                           the cavity, 2 otherwise; lexicographic cavity: 2), 1, 2 or 3 (cavity);
+                           bit-identical either way */
   /* Rayleigh-Benard (case 3), free-fall units: H = 1, U = sqrt(g beta dT H),
    * nu = sqrt(Pr/Ra), kappa = 1/sqrt(Ra Pr); hot bottom wall t_hot, cold top
    * wall t_cold, adiabatic side walls; buoyancy (T - t_ref) on v. */
@@ -101,6 +103,8 @@ typedef struct cfd_timing {
   long long steps;
   long long poisson_sweeps;   /* SOR iterations executed by those launches (up to 3 per fused launch) */
   long long poisson_overlapped; /* pair launches split into interior + halo-overlapped boundary rows (ranks) */
+  double poisson_steady_ms;   /* lexicographic order: device time of the launches with every cell active */
+  long long poisson_steady_launches; /* (the ramps at the start / end of a solve excluded) */
 } cfd_timing;
 
 /* Library / ABI info. */

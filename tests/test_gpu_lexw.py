@@ -1,0 +1,127 @@
+"""The reference's lexicographic SOR order at any grid size on the GPU
+(ordering="lex" for the cavity: csrc/lexw.hpp, the red-black march with the
+i+j time skew), bit for bit against the oracle's restatement of the
+reference's own loop (oracle/ ORC_LEX, pinned to the reference binaries by
+tests/test_oracle_golden.py).
+
+Bars: iteration counts equal, reported residual equal, every field equal bit
+for bit — at capped sweep counts where the solve runs into the cap (the
+BASELINE sizes), at converging solves (the early stop and its replay), on
+1..3 strips, for 1, 2 and 3 sweeps per launch.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import cfd_amd as C  # noqa: E402
+import oracle as O  # noqa: E402
+from test_gpu_parity import assert_bits, ofield  # noqa: E402
+
+
+def solve_both(cp, f, strips=1, spl=0):
+    g = C.CavitySolver(cp, ordering="lex", n_strips=strips, sweeps_per_launch=spl)
+    o = O.Oracle(cp, ordering=O.LEX)
+    g.set_field("src", f)
+    o.field("src")[...] = f
+    ig, rg = g.solverPressurePoisson()
+    io, ro = o.poisson()
+    return g, o, (ig, rg), (io, ro)
+
+
+def random_source(cp, seed=5, scale=10.0):
+    rng = np.random.default_rng(seed)
+    f = np.zeros((cp.ny + 2, cp.nx + 2))
+    f[1:cp.ny + 1, 1:cp.nx + 1] = rng.standard_normal((cp.ny, cp.nx)) * scale
+    return f
+
+
+@pytest.mark.parametrize("spl", [1, 2, 3])
+@pytest.mark.parametrize("nx,ny,K", [(40, 24, 37), (300, 130, 25), (129, 257, 1), (129, 257, 2), (257, 64, 113)])
+def test_capped_solve_bitexact(nx, ny, K, spl):
+    cp = C.make_params("cavity", nx=nx, ny=ny, max_iters=K)
+    f = random_source(cp)
+    g, o, (ig, rg), (io, ro) = solve_both(cp, f, spl=spl)
+    assert ig == io == K
+    assert rg == ro
+    assert_bits(g.field("p"), o.field("p"), f"lexw p {nx}x{ny} K={K} spl={spl}")
+
+
+@pytest.mark.parametrize("strips", [2, 3])
+def test_capped_solve_strips_bitexact(strips):
+    cp = C.make_params("cavity", nx=200, ny=150, max_iters=41)
+    f = random_source(cp, seed=9)
+    g, o, (ig, rg), (io, ro) = solve_both(cp, f, strips=strips)
+    assert (ig, rg) == (io, ro)
+    assert_bits(g.field("p"), o.field("p"), f"lexw strips={strips}")
+
+
+@pytest.mark.parametrize("spl", [2, 3])
+def test_converging_solve_stops_at_reference_iteration(spl):
+    """The reference's own 63² cavity: a realistic source (one predictor step)
+    converges in a few hundred sweeps; the stop is detected up to (nx+ny)/2
+    iterations late and replayed to exactly the reference's count."""
+    cp = C.reference_defaults("cavity")
+    g = C.CavitySolver(cp, ordering="lex", sweeps_per_launch=spl)
+    o = O.Oracle(cp, ordering=O.LEX)
+    g.applyBoundaryConditions()
+    g.computeTentativeVelocities()
+    g.buildSourceTerm()
+    o.velocity_bc(False)
+    o.tentative()
+    o.source()
+    ig, rg = g.solverPressurePoisson()
+    io, ro = o.poisson()
+    assert 10 < io < cp.max_iters
+    assert (ig, rg) == (io, ro)
+    assert_bits(g.field("p"), o.field("p"), "converged p")
+
+
+@pytest.mark.parametrize("case", ["cavity_ref", "cavity_128"])
+def test_whole_steps_bitexact(case):
+    if case == "cavity_ref":
+        cp, steps = C.reference_defaults("cavity"), 12
+    else:  # BASELINE configs[0]
+        cp, steps = C.make_params("cavity", re=100.0, nx=128, ny=128, dt=1e-3), 8
+    g = C.CavitySolver(cp, ordering="lex")
+    o = O.Oracle(cp, ordering=O.LEX)
+    g.applyBoundaryConditions()
+    for k in range(steps):
+        assert g.step() == o.step(), k
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"{case} {name}")
+
+
+def test_cavity_1024_step_bitexact_capped():
+    """BASELINE configs[1] size: whole timesteps in the reference's order."""
+    cp = C.make_params("cavity", re=1000.0, nx=1024, ny=1024, max_iters=150)
+    g = C.CavitySolver(cp, ordering="lex")
+    o = O.Oracle(cp, ordering=O.LEX)
+    g.applyBoundaryConditions()
+    for k in range(2):
+        assert g.step() == o.step(), k
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"1024 {name}")
+
+
+def test_cavity_4096_step_bitexact_capped():
+    """The bench size: one whole timestep in the reference's order (capped)."""
+    cp = C.make_params("cavity", re=1000.0, nx=4096, ny=4096, max_iters=24)
+    g = C.CavitySolver(cp, ordering="lex")
+    o = O.Oracle(cp, ordering=O.LEX)
+    g.applyBoundaryConditions()
+    assert g.step() == o.step()
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"4096 {name}")
+
+
+def test_rayleigh_benard_lex_bitexact():
+    cp = C.make_params("rayleigh_benard", nx=96, ny=32, ra=2e4, max_iters=300)
+    g = C.RayleighBenardSolver(cp, ordering="lex")
+    o = O.Oracle(cp, ordering=O.LEX)
+    for k in range(6):
+        assert g.step() == o.step(), k
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"RB lex {name}")
