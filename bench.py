@@ -77,6 +77,10 @@ def cpu_baseline(nx: int, ny: int, budget_s: float, case: str = "cavity") -> dic
                       f"{nx}x{ny} {case} after one predictor step, {el:.1f} s single-threaded"}
 
 
+def kcase_of(case: str) -> str:
+    return "cavity" if case == "rayleigh_benard" else case  # Rayleigh-Benard runs the cavity SOR kernels
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -95,6 +99,8 @@ def main() -> int:
                     help="residual test every N SOR iterations (1 = the reference's stop rule, at every GPU count)")
     ap.add_argument("--sweeps-per-launch", type=int, default=0,
                     help="red-black SOR iterations fused per kernel launch (0: auto = 3 for the cavity)")
+    ap.add_argument("--ordering", default="rb", choices=["rb", "lex"],
+                    help="SOR sweep order: rb (red-black) or lex (the reference's lexicographic order, bit-identical)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -132,10 +138,10 @@ def main() -> int:
         comm_info = _comm_info(comm)
         rows = strip_rows(rank, world, ny_global) if strong else weak_rows(rank, args.ny)
         solver = C.solver_for(cp, device=local_rank, check_every=check_every, rank_rows=rows, comm=comm,
-                              sweeps_per_launch=args.sweeps_per_launch)
+                              sweeps_per_launch=args.sweeps_per_launch, ordering=args.ordering)
     else:
         solver = C.solver_for(cp, device=local_rank, check_every=check_every,
-                              sweeps_per_launch=args.sweeps_per_launch)
+                              sweeps_per_launch=args.sweeps_per_launch, ordering=args.ordering)
 
     def barrier():
         if world > 1:
@@ -172,7 +178,13 @@ def main() -> int:
         g0, g1 = solver.owned_rows()
         wrows = (g1 - g0 + 1) + (1 if g0 == 1 else 0) + (1 if g1 == cp.ny else 0)
         cells_per_launch = wrows * (cp.nx + 2)
-        avg_launch_ms = tm.poisson_ms / max(tm.poisson_launches, 1)
+        lexw = args.ordering == "lex" and kcase_of(args.case) == "cavity"
+        if lexw and tm.poisson_steady_launches > 0:
+            # lexicographic order: the launches with every cell active (the
+            # ramps at both ends of a solve skip or mask part of the grid)
+            avg_launch_ms = tm.poisson_steady_ms / tm.poisson_steady_launches
+        else:
+            avg_launch_ms = tm.poisson_ms / max(tm.poisson_launches, 1)
         sweeps_per_launch = tm.poisson_sweeps / max(tm.poisson_launches, 1)
         # HBM bytes one launch must move: p_in + f read once, p_out written once,
         # whatever the number of sweeps fused into it
@@ -191,7 +203,7 @@ def main() -> int:
             except Exception:
                 traffic = None
         mlups = updates / elapsed / 1e6
-        kcase = "cavity" if args.case == "rayleigh_benard" else args.case  # RB runs the cavity SOR kernel
+        kcase = kcase_of(args.case)
         rows_here = g1 - g0 + 1
         per_gpu = (f"{cp.nx}x{rows_here} fp64 cells per GPU (global {cp.nx}x{cp.ny} split over {n_gpus} GPUs)"
                    if strong else f"{cp.nx}x{args.ny} fp64 cells per GPU (global {cp.nx}x{cp.ny})")
@@ -214,7 +226,7 @@ def main() -> int:
                             + f", {per_gpu}, reference SOR tolerance {cp.tol_factor:g}*max|src|, "
                             f"cap {cp.max_iters} sweeps/step, {'strong' if strong else 'weak'} scaling",
                 "nx": cp.nx, "ny_per_gpu": rows_here, "global_ny": cp.ny,
-                "parallelism": f"strip{n_gpus}", "check_every": check_every,
+                "parallelism": f"strip{n_gpus}", "check_every": check_every, "ordering": args.ordering,
             },
             "rccl_ranks": comm_info["nranks"] if comm_info else None,
             "transport": (comm_info["transport"] if comm_info else "none (1 GPU)"),
@@ -229,7 +241,8 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": (f"poisson_multi_kernel<{kcase},3>" if sweeps_per_launch > 2.5
+                "kernel": (f"poisson_lexw_kernel<{round(sweeps_per_launch)}>" if lexw
+                           else f"poisson_multi_kernel<{kcase},3>" if sweeps_per_launch > 2.5
                            else f"poisson_multi_kernel<{kcase},2>" if sweeps_per_launch > 1.5
                            else f"poisson_wave_kernel<{kcase}>"),
                 "bytes_per_launch": BYTES_PER_CELL * cells_per_launch,

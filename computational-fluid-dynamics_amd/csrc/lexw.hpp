@@ -37,12 +37,19 @@
 
 namespace cfd {
 
-constexpr int LEXW_SHARDS = 8;  // copies of the exceedance bitset (by block, ~XCD)
+constexpr int LEXW_SHARDS = 8;
+#ifndef CFD_LEXW_W2
+#define CFD_LEXW_W2 2  // waves per SIMD the steady kernel must fit at NS = 2 (tuned on MI355X)
+#endif
+#ifndef CFD_LEXW_W3
+#define CFD_LEXW_W3 2  // the same at NS = 3
+#endif
+#define CFD_LEXW_MIN_WAVES(NS) ((NS) <= 2 ? CFD_LEXW_W2 : CFD_LEXW_W3)  // copies of the exceedance bitset (by block, ~XCD)
 
 struct LexCtl {
-  unsigned long long* bits;  // LEXW_SHARDS x words; bit q of the bitset <-> slot kmax - q
+  unsigned long long* bits;  // LEXW_SHARDS x words; bit q of the bitset <-> iteration q - kmax
   int words;                 // per shard
-  int kmax;                  // slot of bit 0
+  int kmax;                  // offset: bit of iteration k is k + kmax (>= 0 for every iteration a wave touches)
   const double* tol;         // [0] tolerance, [1] initial residual
   int* stop;                 // [0] converged flag, [1] iteration
 };
@@ -50,7 +57,7 @@ struct LexCtl {
 // slot k has a cell whose |residual| exceeds the tolerance (valid once every
 // cell has contributed)
 __device__ __forceinline__ bool lexw_slot_exceeds(const LexCtl& L, int k) {
-  const int q = L.kmax - k;
+  const int q = L.kmax + k;
   unsigned long long w = 0;
 #pragma unroll
   for (int s = 0; s < LEXW_SHARDS; ++s) w |= L.bits[(size_t)s * L.words + (q >> 6)];
@@ -78,17 +85,33 @@ __device__ __forceinline__ bool lexw_go_on(const LexCtl& L, int ka, int kb, bool
 #define LX_SLOT(X) ((((ROT) + 4 - (X)) % 5 + 10) % 5)
 #define LX_S10(X) ((((6 * (ROT) + 5 * (PAR)) % 10 + 9 - (X)) % 10 + 20) % 10)
 
+// The march goes DOWN (row R - X*d with d = -1: ring position X holds row
+// R + X). Sweep S: red at R+2S+1, black at R+2S+2. Marching down, every value
+// a residual of the reference's iteration k needs is at hand while a row is
+// updated, so no extra state is kept:
+//  * red cell c of row jb = R+2S+2 (iteration of half-sweep H0+2S) during
+//    black(S) of row jb: its W (black, before black(S)) and E (black, after)
+//    are the old and new values of this very update; N = row jb+1 (black(S)
+//    done one step earlier); S = row jb-1 (red(S) done, black(S) not yet);
+//  * black cell c' of row jr = R+2S+1 (iteration of half-sweep H0+2S-1)
+//    during red(S) of row jr: W', E' = the old / new red values; N' = row
+//    jr+1 (red(S) done); S' = row jr-1 (sweep S's front row, red(S) not yet).
+//    For S = 0 these are the previous launch's last black half-sweep.
+// Lane l's contributions at front row R all belong to the same iteration,
+// Bd(R) - l with Bd(R) = (H0 - c0 - R - (R&1) - 2)/2 + 1 (sweeps and colours
+// alike): at march step t (R = Rbeg - t, Rbeg even) that is Bd0 + t/2 - l. A
+// step's residuals are max-reduced in registers, compared with the tolerance
+// once, and recorded as bit t/2 of a per-lane mask (VALU only: scalar work in
+// the march stalls the wave); the lanes' masks are merged along the
+// diagonals (iteration = Bd0 + t/2 - l) once per wave.
+
 template <int NS>
 struct LexRun {
-  double2 w[NS][5];   // sweep S: latest values of rows R-2S .. R-2S-4
-  double2 in[NS][5];  // sweep S: the same rows as they entered sweep S
-  double2 fr[10];     // source rows R-1 .. R-10
-  double2 np[5];      // prefetched p_in rows R .. R+4
-  double2 nf[5];      // prefetched f rows R-1 .. R+3
-  // exceedance bits, wave-uniform: window bit b <-> slot top - b; bits that
-  // leave the window (slot top) are appended to hist (bit e: e-th emission)
-  unsigned long long win0, win1, hist0, hist1;
-  int top, nemit;
+  double2 w[NS][5];  // sweep S: rows R+2S .. R+2S+4
+  double2 fr[10];    // source rows R+1 .. R+10
+  double2 np[5];     // prefetched p_in rows R .. R-4
+  double2 nf[5];     // prefetched f rows R+1 .. R-3
+  unsigned long long mask;  // bit t/2: a residual of this lane's iteration Bd0 + t/2 - lane exceeds tol
 };
 
 // Per-wave context beyond WaveCtx: the launch's half-sweeps and the cap.
@@ -96,239 +119,232 @@ struct LexCtx {
   int H0;    // first half-sweep of the launch (even: red)
   int K;     // iterations every cell performs (the cap, or the replayed count)
   double tol;
+  double o2, o3, o4;  // omega / nc (Coef::om_nc) held as values: a select of
+                      // Coef fields becomes a select of addresses and a load
 };
 
-// one red-black half-sweep update of row j (ring slot X), colour COLOR
-// (0 red, 1 black) at half-sweep H; MASK: per-cell activity and walls
-template <int ROT, int JPAR, int COLOR, bool MASK>
-__device__ __forceinline__ void lx_update(const WaveCtx<CAVITY>& x, const LexCtx& lc, double2 (&W)[5], int j, int X,
-                                          int H, const double2& fc) {
+// Row R of a field at this lane's column pair, row and column clamped to
+// stored memory and no select on the value (a select would wait for the load
+// and defeat the prefetch): values of rows / lanes outside the grid only feed
+// cells that are never updated (ghost rows and columns, halo edges) and are
+// never stored.
+__device__ __forceinline__ double2 lx_ld(const WaveCtx<CAVITY>& x, const double* base, int R) {
+  const int Rc = min(max(R, x.rmin), x.rmax);
+  return *reinterpret_cast<const double2*>(base + (size_t)(Rc - x.g.row_lo) * (size_t)x.g.pitch + x.gic);
+}
+
+// MODE LX_ACT: per-cell activity masks (tiles on the ramps); 0: every cell
+// active in every half-sweep of the launch. Wall columns (the first and last
+// column tile, `edge`) take wave-uniform branches inside the same code.
+constexpr int LX_ACT = 1;
+template <int MODE>
+__device__ __forceinline__ bool lx_active(const LexCtx& lc, int s, int H) {
+  return !(MODE & LX_ACT) || (s <= H && H <= s + 2 * (lc.K - 1));
+}
+
+// SOR update (cavity-01.cpp:643-654). The solve's field starts at zero with
+// +0.0 ghosts that never change, so a wall's indicator product 0*p_ghost is
+// +0.0 = p_ghost itself: only omega/nc differs at the walls (nc = 4 - walls
+// among W, E, N; es = 1 always). Row-uniform j == ny, lane-constant wall.
+// Ghost / outside columns of an edge tile are not updated: omega/nc = 0 and
+// 1 - omega = 1 there give pc + 0*(finite) = pc (+0.0 ghosts stay +0.0).
+__device__ __forceinline__ double lx_upd(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool edge, int j, int i,
+                                         double pc, double pW, double pE, double pS, double pN, double fc) {
+  const Coef& c = x.c;
+  const double sum = (pE + pW) + (pN + pS) - fc * c.h2;
+  const bool top = j == x.g.ny;  // row-uniform
+  if (!edge) return pc * c.one_m_omega + (top ? lc.o3 : lc.o4) * sum;
+  const bool in = i >= 1 && i <= x.g.nx;
+  const bool wall = (i == 1) || (i == x.g.nx);
+  const double omw = top ? lc.o2 : lc.o3, omi = top ? lc.o3 : lc.o4;
+  const double om = !in ? 0.0 : wall ? omw : omi;
+  const double omm = in ? c.one_m_omega : 1.0;
+  return pc * omm + om * sum;
+}
+
+// |residual| (cavity-01.cpp:659-677) with the indicator products as selects
+// (residual_abs): the same |r| bits.
+__device__ __forceinline__ double lx_res(const WaveCtx<CAVITY>& x, bool edge, int j, int i, double pc, double pW,
+                                         double pE, double pS, double pN, double fc) {
+  if (!edge && j != x.g.ny) return residual_interior<CAVITY>(x.c, pc, pW, pE, pS, pN, fc);
+  const double tE = (!edge || i < x.g.nx) ? (pE - pc) : 0.0;
+  const double tW = (!edge || i > 1) ? (pW - pc) : 0.0;
+  const double tN = (j < x.g.ny) ? (pN - pc) : 0.0;
+  const double tS = pS - pc;
+  return fabs(x.c.idx2 * (tE + tW + tN + tS) - fc);
+}
+
+// Update of row j = R + X (colour COLOR at half-sweep H) and, from the old and
+// new values, |residual| of the other colour's cell of this lane (iteration of
+// half-sweep H-1; 0 for rows outside the wave's output rows and, in edge /
+// ramp tiles, for cells outside the grid or inactive at H-1).
+template <int ROT, int JPAR, int COLOR, int MODE, bool STORE>
+__device__ __forceinline__ double lx_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool edge, double2 (&W)[5], int j,
+                                       int X, int H, const double2& fc) {
   double2& m = W[LX_SLOT(X)];
-  const double2 bh = W[LX_SLOT(X + 1)], ah = W[LX_SLOT(X - 1)];  // rows j-1 (S), j+1 (N)
-  if (!(j > x.rmin && j < x.rmax)) return;                         // row-uniform
-  if (((JPAR ^ COLOR) & 1) == 0) {  // slot a (even column gi) has this colour
-    const double Lb = dpp_from_left(m.y);
-    if (MASK) {
-      const double nv = sor_update<CAVITY>(x.c, x.g.nx, x.g.ny, j, x.gi, m.x, Lb, m.y, bh.x, ah.x, fc.x);
-      const int s = x.gi + j;
-      m.x = (x.fl_a(j) && s <= H && H <= s + 2 * (lc.K - 1)) ? nv : m.x;
+  const double2 nb = W[LX_SLOT(X + 1)], sb = W[LX_SLOT(X - 1)];  // rows j+1 (N), j-1 (S)
+  const double2 old = m;
+  const bool upd = j > x.rmin && j < x.rmax;  // row-uniform
+  // this colour's slot: a (even column gi) iff (j + COLOR) even
+  constexpr bool A = ((JPAR ^ COLOR) & 1) == 0;
+  if (upd) {  // (rows 1..ny: rmin/rmax exclude the ghost rows)
+    if (A) {
+      const double Lb = dpp_from_left(m.y);
+      const double nv = lx_upd(x, lc, edge, j, x.gi, m.x, Lb, m.y, sb.x, nb.x, fc.x);
+      m.x = lx_active<MODE>(lc, x.gi + j, H) ? nv : m.x;
     } else {
-      m.x = sor_fast<CAVITY>(x, j, m.x, Lb, m.y, bh.x, ah.x, fc.x);
-    }
-  } else {
-    const double Ra = dpp_from_right(m.x);
-    if (MASK) {
-      const double nv = sor_update<CAVITY>(x.c, x.g.nx, x.g.ny, j, x.gi + 1, m.y, m.x, Ra, bh.y, ah.y, fc.y);
-      const int s = x.gi + 1 + j;
-      m.y = (x.fl_b(j) && s <= H && H <= s + 2 * (lc.K - 1)) ? nv : m.y;
-    } else {
-      m.y = sor_fast<CAVITY>(x, j, m.y, m.x, Ra, bh.y, ah.y, fc.y);
+      const double Ra = dpp_from_right(m.x);
+      const double nv = lx_upd(x, lc, edge, j, x.gi + 1, m.y, m.x, Ra, sb.y, nb.y, fc.y);
+      m.y = lx_active<MODE>(lc, x.gi + 1 + j, H) ? nv : m.y;
     }
   }
-}
-
-// |cavity residual| (cavity-01.cpp:659-677) of cell (j, i); interior cells
-// below the top row need no indicators
-template <bool MASK>
-__device__ __forceinline__ double lx_res(const WaveCtx<CAVITY>& x, int j, int i, double pc, double pW, double pE,
-                                         double pS, double pN, double fc) {
-  if (MASK || j == x.g.ny) return residual_abs<CAVITY>(x.c, x.g.nx, x.g.ny, j, i, pc, pW, pE, pS, pN, fc);
-  return residual_interior<CAVITY>(x.c, pc, pW, pE, pS, pN, fc);
-}
-
-// Residual stage of sweep S at row j = R - (2S+3): red cells of iteration
-// H0+2S, black cells of H0+2S-1 (the previous sweep); one ballot each into
-// the exceedance window; the last sweep also stores row j.
-template <int S, int NS, int ROT, int PAR, bool MASK>
-__device__ __forceinline__ void lx_residual(const WaveCtx<CAVITY>& x, const LexCtx& lc, LexRun<NS>& s, int R,
-                                            int lane) {
-  const int j = R - (2 * S + 3);
-  constexpr int JP = PAR ^ 1;  // parity of j
-  const double2 m = s.w[S][LX_SLOT(2 * S + 3)];   // row j, after sweep S
-  const double2 nN = s.w[S][LX_SLOT(2 * S + 2)];  // row j+1, after sweep S
-  const double2 ij = s.in[S][LX_SLOT(2 * S + 3)];  // row j, before sweep S
-  const double2 is = s.in[S][LX_SLOT(2 * S + 4)];  // row j-1, before sweep S
-  const double2 fc = s.fr[LX_S10(2 * S + 3)];
-  if (!(j >= x.y0 && j < x.y1)) return;  // row-uniform
-  if (S == NS - 1 && x.out_lane) {
+  if (STORE && j >= x.y0 && j < x.y1 && x.out_lane) {
     double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
     typedef double d2v __attribute__((ext_vector_type(2)));
     d2v mv = {m.x, m.y};
     __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
   }
-  if (!(j >= x.g.j0 && j <= x.g.j1)) return;
-  const double Lin = dpp_from_left(ij.y);  // lane l-1, column gi-1, before sweep S
-  const double Rfi = dpp_from_right(m.x);  // lane l+1, column gi+2, after sweep S
-  double rr, rb;                           // |r| of the red and the black cell of this lane
-  int ir, ib;
-  if (JP == 0) {  // red at gi (slot a), black at gi+1 (slot b)
-    ir = x.gi;
-    ib = x.gi + 1;
-    rr = lx_res<MASK>(x, j, ir, m.x, Lin, m.y, is.x, nN.x, fc.x);
-    rb = lx_res<MASK>(x, j, ib, ij.y, ij.x, Rfi, is.y, nN.y, fc.y);
-  } else {  // red at gi+1 (slot b), black at gi (slot a)
-    ir = x.gi + 1;
-    ib = x.gi;
-    rr = lx_res<MASK>(x, j, ir, m.y, ij.x, Rfi, is.y, nN.y, fc.y);
-    rb = lx_res<MASK>(x, j, ib, ij.x, Lin, m.y, is.x, nN.x, fc.x);
+  // residual of the other colour's cell of this lane (iteration of half-sweep H-1)
+  if (!(j >= x.y0 && j < x.y1 && j >= x.g.j0 && j <= x.g.j1)) return 0.0;  // row-uniform
+  double r;
+  int i;
+  if (A) {  // updated: slot a (gi); the other colour is at gi+1: W = gi (old), E = gi+2 (lane l+1, new)
+    i = x.gi + 1;
+    const double E = dpp_from_right(m.x);
+    r = lx_res(x, edge, j, i, m.y, old.x, E, sb.y, nb.y, fc.y);
+  } else {  // updated: slot b (gi+1); the other colour is at gi: W = gi-1 (lane l-1, old), E = gi+1 (new)
+    i = x.gi;
+    const double Wv = dpp_from_left(old.y);
+    r = lx_res(x, edge, j, i, m.x, Wv, m.y, sb.x, nb.x, fc.x);
   }
-  bool pr = x.out_lane && rr > lc.tol;
-  bool pb = x.out_lane && rb > lc.tol;
-  if (MASK) {  // interior cells only, and iterations 1..K
-    const int H = lc.H0 + 2 * S;
-    const int kr = (H - (ir + j)) / 2 + 1, kb = (H - 1 - (ib + j)) / 2 + 1;
-    pr = pr && ir >= 1 && ir <= x.g.nx && (H - (ir + j)) >= 0 && kr <= lc.K;
-    pb = pb && ib >= 1 && ib <= x.g.nx && (H - 1 - (ib + j)) >= 0 && kb <= lc.K;
-  }
-  const unsigned long long mr = __ballot(pr), mb = __ballot(pb);
-  // window bit of lane 0's red slot: 2NS - 2S; black: +1 on even rows
-  constexpr int br = 2 * NS - 2 * S, bb = br + (JP == 0 ? 1 : 0);
-  s.win0 |= mr << br;
-  s.win1 |= mr >> (64 - br);
-  s.win0 |= mb << bb;
-  s.win1 |= mb >> (64 - bb);
+  if (edge) r = (i >= 1 && i <= x.g.nx) ? r : 0.0;
+  if (MODE & LX_ACT) r = lx_active<MODE>(lc, i + j, H - 1) ? r : 0.0;
+  return r;
 }
 
-template <int S, int NS, int ROT, int PAR, bool MASK>
-__device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, LexRun<NS>& s, int R, int lane) {
+template <int S, int NS, int ROT, int PAR, int MODE>
+__device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool edge, LexRun<NS>& s, int R,
+                                          double& rs) {
   if constexpr (S < NS) {
-    if constexpr (S == 0) s.in[0][LX_SLOT(0)] = s.w[0][LX_SLOT(0)];
-    // red at R-(2S+1) (parity PAR^1) in half-sweep H0+2S, black at R-(2S+2) in H0+2S+1
-    lx_update<ROT, PAR ^ 1, 0, MASK>(x, lc, s.w[S], R - (2 * S + 1), 2 * S + 1, lc.H0 + 2 * S,
-                                     s.fr[LX_S10(2 * S + 1)]);
-    lx_update<ROT, PAR, 1, MASK>(x, lc, s.w[S], R - (2 * S + 2), 2 * S + 2, lc.H0 + 2 * S + 1,
-                                 s.fr[LX_S10(2 * S + 2)]);
-    lx_residual<S, NS, ROT, PAR, MASK>(x, lc, s, R, lane);
-    if constexpr (S + 1 < NS) {
-      s.w[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
-      s.in[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
-    }
-    lx_sweeps<S + 1, NS, ROT, PAR, MASK>(x, lc, s, R, lane);
+    // red at R+2S+1 (parity PAR^1) in half-sweep H0+2S; black at R+2S+2 (PAR) in H0+2S+1
+    rs = fmax(rs, lx_row<ROT, PAR ^ 1, 0, MODE, false>(x, lc, edge, s.w[S], R + 2 * S + 1, 2 * S + 1, lc.H0 + 2 * S,
+                                                       s.fr[LX_S10(2 * S + 1)]));
+    rs = fmax(rs, lx_row<ROT, PAR, 1, MODE, S == NS - 1>(x, lc, edge, s.w[S], R + 2 * S + 2, 2 * S + 2,
+                                                         lc.H0 + 2 * S + 1, s.fr[LX_S10(2 * S + 2)]));
+    if constexpr (S + 1 < NS) s.w[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
+    lx_sweeps<S + 1, NS, ROT, PAR, MODE>(x, lc, edge, s, R, rs);
   }
 }
 
-template <int NS, int ROT, int PAR, bool MASK>  // PAR = parity of R
-__device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& lc, LexRun<NS>& s, int R, int lane) {
-  if constexpr (PAR == 0) {
-    // residual slots move down by one every two rows: the window's top slot
-    // is final for this wave
-    const unsigned long long e = s.win0 & 1ull;
-    if (s.nemit < 64) s.hist0 |= e << s.nemit;
-    else s.hist1 |= e << (s.nemit - 64);
-    s.nemit++;
-    s.win0 = (s.win0 >> 1) | (s.win1 << 63);
-    s.win1 >>= 1;
-    s.top--;
-  }
+template <int NS, int ROT, int PAR, int MODE>  // PAR = parity of R
+__device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool edge, LexRun<NS>& s, int R,
+                                        unsigned long long bit) {
   s.w[0][LX_SLOT(0)] = s.np[LX_SLOT(0)];
   s.fr[LX_S10(1)] = s.nf[LX_SLOT(0)];
-  if (MASK) {
-    s.np[LX_SLOT(-4)] = x.ld(x.pin, R + 4);
-    s.nf[LX_SLOT(-4)] = x.ld(x.f, R + 3);
-  } else {
-    s.np[LX_SLOT(-4)] = x.ld_fast(x.pin, R + 4);
-    s.nf[LX_SLOT(-4)] = x.ld_fast(x.f, R + 3);
-  }
-  lx_sweeps<0, NS, ROT, PAR, MASK>(x, lc, s, R, lane);
+  s.np[LX_SLOT(-4)] = lx_ld(x, x.pin, R - 4);
+  s.nf[LX_SLOT(-4)] = lx_ld(x, x.f, R - 3);
+  double rs = 0.0;
+  lx_sweeps<0, NS, ROT, PAR, MODE>(x, lc, edge, s, R, rs);
+  s.mask |= (rs > lc.tol) ? bit : 0ull;
 }
 
-// OR `len` bits (bits[0..3], 256 max) into shard `sh` of the bitset at bit q0
-__device__ __forceinline__ void lexw_flush(const LexCtl& L, int sh, int q0, const unsigned long long (&b)[4], int len) {
+// OR across the wave's 64 lanes
+__device__ __forceinline__ unsigned long long wave_or64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+    v |= (unsigned long long)(unsigned)__shfl_xor((int)lo, off, 64) |
+         ((unsigned long long)(unsigned)__shfl_xor((int)hi, off, 64) << 32);
+  }
+  return v;
+}
+
+// OR `len` bits (b[0..2], 192 max) into shard `sh` of the bitset at bit q0 >= 0
+__device__ __forceinline__ void lexw_flush(const LexCtl& L, int sh, int q0, const unsigned long long (&b)[3], int len) {
   unsigned long long* G = L.bits + (size_t)sh * L.words;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < 3; ++c) {
     if (c * 64 >= len || b[c] == 0) continue;
     const int q = q0 + c * 64;
-    const int w = q >> 6, o = q & 63;  // (q0 >= 0: slots <= kmax)
-    if (w >= 0 && w < L.words) atomicOr(&G[w], b[c] << o);
-    if (o && w + 1 >= 0 && w + 1 < L.words) atomicOr(&G[w + 1], b[c] >> (64 - o));
+    const int w = q >> 6, o = q & 63;
+    if (w < L.words) atomicOr(&G[w], b[c] << o);
+    if (o && w + 1 < L.words) atomicOr(&G[w + 1], b[c] >> (64 - o));
   }
 }
 
-template <int NS, bool MASK>
-__device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L, int y0, int y1,
-                                         int c0, int lane, int shard) {
+template <int NS, int MODE>
+__device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L, bool edge, int y0,
+                                         int y1, int c0, int lane, int shard) {
   constexpr int H = 2 * NS + 1;
-  const int Rb0 = y0 - H;
-  const int Rbeg = Rb0 - (Rb0 & 1);  // even first front row: compile-time colours
+  const int Rb0 = y1 - 1 + H;
+  const int Rbeg = Rb0 + (Rb0 & 1);  // even first front row: compile-time colours
   const int nsteps = (y1 - y0) + 2 * H + (Rb0 & 1);
   LexRun<NS> s;
   const double2 z = make_double2(0.0, 0.0);
 #pragma unroll
   for (int k = 0; k < 5; ++k)
 #pragma unroll
-    for (int q = 0; q < NS; ++q) s.w[q][k] = s.in[q][k] = z;
+    for (int q = 0; q < NS; ++q) s.w[q][k] = z;
 #pragma unroll
   for (int k = 0; k < 10; ++k) s.fr[k] = z;
   {
     constexpr int ROT = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      s.np[LX_SLOT(-q)] = MASK ? x.ld(x.pin, Rbeg + q) : x.ld_fast(x.pin, Rbeg + q);
-      s.nf[LX_SLOT(-q)] = MASK ? x.ld(x.f, Rbeg + (q - 1)) : x.ld_fast(x.f, Rbeg + (q - 1));
+      s.np[LX_SLOT(-q)] = lx_ld(x, x.pin, Rbeg - q);
+      s.nf[LX_SLOT(-q)] = lx_ld(x, x.f, Rbeg - (q - 1));
     }
   }
-  // slot of lane 0's red cell at sweep 0 in the residual stage of front row R:
-  // B(R) = (H0 - c0 - R + 3 - ((R+1)&1))/2 + 1; window top = B + 2NS, taken
-  // one row early because even steps shift first
-  s.top = (lc.H0 - c0 - (Rbeg - 2) + 3 - ((Rbeg - 1) & 1)) / 2 + 1 + 2 * NS;
-  s.win0 = s.win1 = s.hist0 = s.hist1 = 0ull;
-  s.nemit = 0;
-  const int top0 = s.top;
+  s.mask = 0ull;
   int R = Rbeg;
-  for (int st = 0; st < nsteps; st += 10, R += 10) {
-    lx_step<NS, 0, 0, MASK>(x, lc, s, R, lane);
-    lx_step<NS, 1, 1, MASK>(x, lc, s, R + 1, lane);
-    lx_step<NS, 2, 0, MASK>(x, lc, s, R + 2, lane);
-    lx_step<NS, 3, 1, MASK>(x, lc, s, R + 3, lane);
-    lx_step<NS, 4, 0, MASK>(x, lc, s, R + 4, lane);
-    lx_step<NS, 0, 1, MASK>(x, lc, s, R + 5, lane);
-    lx_step<NS, 1, 0, MASK>(x, lc, s, R + 6, lane);
-    lx_step<NS, 2, 1, MASK>(x, lc, s, R + 7, lane);
-    lx_step<NS, 3, 0, MASK>(x, lc, s, R + 8, lane);
-    lx_step<NS, 4, 1, MASK>(x, lc, s, R + 9, lane);
+  // (nsteps + 9 <= 127 by the host's band limit: bits t/2 < 64)
+#define LX_BIT(T) ((((st + (T)) >> 1) < 64) ? (1ull << ((st + (T)) >> 1)) : 0ull)
+  for (int st = 0; st < nsteps; st += 10, R -= 10) {
+    lx_step<NS, 0, 0, MODE>(x, lc, edge, s, R, LX_BIT(0));
+    lx_step<NS, 1, 1, MODE>(x, lc, edge, s, R - 1, LX_BIT(1));
+    lx_step<NS, 2, 0, MODE>(x, lc, edge, s, R - 2, LX_BIT(2));
+    lx_step<NS, 3, 1, MODE>(x, lc, edge, s, R - 3, LX_BIT(3));
+    lx_step<NS, 4, 0, MODE>(x, lc, edge, s, R - 4, LX_BIT(4));
+    lx_step<NS, 0, 1, MODE>(x, lc, edge, s, R - 5, LX_BIT(5));
+    lx_step<NS, 1, 0, MODE>(x, lc, edge, s, R - 6, LX_BIT(6));
+    lx_step<NS, 2, 1, MODE>(x, lc, edge, s, R - 7, LX_BIT(7));
+    lx_step<NS, 3, 0, MODE>(x, lc, edge, s, R - 8, LX_BIT(8));
+    lx_step<NS, 4, 1, MODE>(x, lc, edge, s, R - 9, LX_BIT(9));
   }
-  // emitted bits (slots top0 - 1 - e: the first emission is the initial top's
-  // bit 0... see below), then the window: one descending run of slots
-  // position p <-> slot (top0 - 1) - p... the first shift happens at step 0
-  // (R even), emitting bit 0 of the empty window for slot top0 - 0; so
-  // position p <-> slot top0 - p for p < nemit, and window bit b <-> slot
-  // s.top - b = top0 - nemit - b: position nemit + b. One run, slots descending.
-  unsigned long long b[4];
-  const int n = s.nemit;  // <= 128
-  // b = hist (n bits) | window << n
-  b[0] = s.hist0;
-  b[1] = s.hist1;
-  b[2] = 0ull;
-  b[3] = 0ull;
-  {
-    const int w = n >> 6, o = n & 63;
-    unsigned long long v0 = s.win0, v1 = s.win1;
-    // OR (v1:v0) << n into b
-    if (w == 0) {
-      b[0] |= v0 << o;
-      b[1] |= o ? ((v0 >> (64 - o)) | (v1 << o)) : v1;
-      b[2] |= o ? (v1 >> (64 - o)) : 0ull;
-    } else if (w == 1) {
-      b[1] |= v0 << o;
-      b[2] |= o ? ((v0 >> (64 - o)) | (v1 << o)) : v1;
-      b[3] |= o ? (v1 >> (64 - o)) : 0ull;
-    } else {
-      b[2] |= v0 << o;
-      b[3] |= o ? ((v0 >> (64 - o)) | (v1 << o)) : v1;
-    }
-  }
-  if (lane == 0) lexw_flush(L, shard, L.kmax - top0, b, n + 128);
+#undef LX_BIT
+  // lane l's bit u <-> iteration Bd0 + u - l = (Bd0 - 63) + (u + 63 - l):
+  // shift each lane's mask by 63 - l into a 128-bit run and OR the lanes
+  const unsigned long long m = x.out_lane ? s.mask : 0ull;
+  const int sh = 63 - lane;
+  const unsigned long long lo = m << sh, hi = sh ? (m >> (64 - sh)) : 0ull;
+  unsigned long long b[3] = {wave_or64(lo), wave_or64(hi), 0ull};
+  const int Bd0 = (lc.H0 - c0 - Rbeg - 2) / 2 + 1;
+  if (lane == 0) lexw_flush(L, shard, Bd0 - 63 + L.kmax, b, 128);
+}
+
+// Owned rows of column tile `ct` whose output cells launch H0 touches: a cell
+// (j,i) is updated in one of the launch's half-sweeps or has its black
+// residual of half-sweep H0-1 evaluated (i+j <= H0+2NS-1 and i+j+2(K-1) >=
+// H0-1), or finished in the previous launch and must be copied into this
+// launch's output buffer (i+j+2(K-1) >= H0-2NS). Other rows hold their final
+// values in both buffers already.
+__host__ __device__ inline void lexw_rows(const Geo& g, int H0, int K, int ns, int ct, int* lo, int* hi) {
+  const int cmin = max(ct * PAIR_TWC, 1), cmax = min(ct * PAIR_TWC + PAIR_TWC - 1, g.nx);
+  *lo = max(g.j0, H0 - 2 * ns - 2 * (K - 1) - cmax);
+  *hi = min(g.j1, H0 + 2 * ns - 1 - cmin);
 }
 
 // One launch of NS lexicographic-order sweeps (half-sweeps H0 .. H0+2NS-1) on
-// one strip, tiled as poisson_multi_kernel (PairPlan, interior column tiles
-// use the unmasked march when their whole region is active throughout).
-template <int NS>
-__global__ __launch_bounds__(256, 2) void poisson_lexw_kernel(Geo g, Coef c, const double* __restrict__ pin,
+// one strip, tiled as poisson_multi_kernel (PairPlan). RAMP = false: a launch
+// in which every cell is active in every half-sweep (no activity masks: 4
+// waves per SIMD); RAMP = true: the launches at the start and the end of the
+// solve, whose tiles take the masked marches unless wholly active (the masked
+// code would cost the steady kernel registers, so it lives in its own kernel).
+template <int NS, bool RAMP>
+__global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisson_lexw_kernel(Geo g, Coef c, const double* __restrict__ pin,
                                                               double* __restrict__ pout, const double* __restrict__ f,
                                                               LexCtl L, int H0, int K, int ka, int kb, PairPlan pl,
-                                                              int flags) {
+                                                              int flags, int rth, int rthe) {
   constexpr int CH = 8;  // column halo (lanes 0-3 and 60-63)
   constexpr int H = 2 * NS + 1;
   const int lane = threadIdx.x & 63;
@@ -340,40 +356,59 @@ __global__ __launch_bounds__(256, 2) void poisson_lexw_kernel(Geo g, Coef c, con
   const int bl = (int)blockIdx.x;
   const int blk = (bl < L8) ? (bl % 8) * (nblk / 8) + bl / 8 : bl;
   const int tile = blk * 4 + wv;
-  const int ne = (pl.ctiles >= 2) ? 2 : 1;
-  const int nbe = pl.nbe0 + pl.nbe1, nbi = pl.nb0 + pl.nb1;
-  int band, ctile, th, nb0;
-  if (tile < ne * nbe) {
-    ctile = (tile < nbe) ? 0 : pl.ctiles - 1;
-    band = tile % nbe;
-    th = pl.the;
-    nb0 = pl.nbe0;
+  int ctile, y0, y1;
+  if (rth > 0) {  // ramp launch: only the rows this launch touches, per column tile (lexw_rows)
+    int t = tile;
+    for (ctile = 0; ctile < pl.ctiles; ++ctile) {
+      int lo, hi;
+      lexw_rows(g, H0, K, NS, ctile, &lo, &hi);
+      const int th = (ctile == 0 || ctile == pl.ctiles - 1) ? rthe : rth;
+      const int nb = hi >= lo ? (hi - lo + th) / th : 0;
+      if (t < nb) {
+        y0 = lo + t * th;
+        y1 = min(y0 + th, hi + 1);
+        break;
+      }
+      t -= nb;
+    }
+    if (ctile >= pl.ctiles) return;
   } else {
-    const int t = tile - ne * nbe;
-    const int nci = pl.ctiles - ne;
-    if (t >= nci * nbi) return;
-    ctile = 1 + t % nci;
-    band = t / nci;
-    th = pl.th;
-    nb0 = pl.nb0;
+    const int ne = (pl.ctiles >= 2) ? 2 : 1;
+    const int nbe = pl.nbe0 + pl.nbe1, nbi = pl.nb0 + pl.nb1;
+    int band, th, nb0;
+    if (tile < ne * nbe) {
+      ctile = (tile < nbe) ? 0 : pl.ctiles - 1;
+      band = tile % nbe;
+      th = pl.the;
+      nb0 = pl.nbe0;
+    } else {
+      const int t = tile - ne * nbe;
+      const int nci = pl.ctiles - ne;
+      if (t >= nci * nbi) return;
+      ctile = 1 + t % nci;
+      band = t / nci;
+      th = pl.th;
+      nb0 = pl.nb0;
+    }
+    const bool r0 = band < nb0;
+    y0 = r0 ? pl.lo0 + band * th : pl.lo1 + (band - nb0) * th;
+    y1 = min(y0 + th, r0 ? pl.hi0 : pl.hi1);
   }
   const int c0 = ctile * PAIR_TWC - CH;
   const int gi = c0 + 2 * lane;
-  const bool r0 = band < nb0;
-  const int y0 = r0 ? pl.lo0 + band * th : pl.lo1 + (band - nb0) * th;
-  const int y1 = min(y0 + th, r0 ? pl.hi0 : pl.hi1);
   if (y0 >= y1) return;
 
-  // activity of the marched region (rows y0-H .. y1-1+H, columns c0 .. c0+127,
-  // interior cells only) over this launch's half-sweeps
-  const int rlo = max(max(y0 - H, 1), g.row_lo), rhi = min(min(y1 - 1 + H, g.ny), g.row_lo + g.nrows - 1);
+  // activity of the marched region (rows y0-H-1 .. y1+H, columns c0 .. c0+127,
+  // interior cells) over this launch's half-sweeps (and the previous launch's
+  // last one, whose black residuals this launch evaluates)
+  const int rlo = max(max(y0 - H - 1, 1), g.row_lo), rhi = min(min(y1 + H, g.ny), g.row_lo + g.nrows - 1);
   const int clo = max(c0, 1), chi = min(c0 + 127, g.nx);
   const int smin = clo + rlo, smax = chi + rhi;
   const int Hend = H0 + 2 * NS - 1;
   const int last = 2 * (K - 1);
-  if (smin > Hend) return;                 // not started: both buffers hold the initial field
-  if (smax + last < H0 - 2 * NS) return;   // finished two launches ago: both buffers hold the result
-  const bool full = smax <= H0 && smin + last >= Hend && clo == c0 && chi == c0 + 127;
+  if (smin > Hend) return;                // not started: both buffers hold the initial field
+  if (smax + last < H0 - 2 * NS) return;  // finished before the previous launch: both hold the result
+  const bool cols_in = clo == c0 && chi == c0 + 127;
 
   WaveCtx<CAVITY> x{g, c};
   x.pin = pin; x.pout = pout; x.f = f;
@@ -388,10 +423,12 @@ __global__ __launch_bounds__(256, 2) void poisson_lexw_kernel(Geo g, Coef c, con
   x.icol_b = gi + 1 >= 1 && gi + 1 <= g.nx;
   x.open_a = x.open_b = true;
   x.gic = min(max(gi, 0), g.pitch - 2);
-  LexCtx lc{H0, K, L.tol[0]};
+  LexCtx lc{H0, K, L.tol[0], c.om_nc[2], c.om_nc[3], c.om_nc[4]};
+  asm("" : "+s"(lc.o2), "+s"(lc.o3), "+s"(lc.o4));
   const int shard = bl & (LEXW_SHARDS - 1);
-  if (full) lx_march<NS, false>(x, lc, L, y0, y1, c0, lane, shard);
-  else lx_march<NS, true>(x, lc, L, y0, y1, c0, lane, shard);
+  const bool edge = !cols_in;
+  if constexpr (RAMP) lx_march<NS, LX_ACT>(x, lc, L, edge, y0, y1, c0, lane, shard);
+  else lx_march<NS, 0>(x, lc, L, edge, y0, y1, c0, lane, shard);
 }
 
 #undef LX_SLOT

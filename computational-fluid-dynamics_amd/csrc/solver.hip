@@ -203,10 +203,12 @@ class Solver {
       if (const char* e = std::getenv("CFD_PAIR_WPS")) pps = std::max(1, std::atoi(e));
       if (use_lexw()) {
         int lps = 0;
-        if (lexw_ns() == 1) HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<1>, 256, 0));
-        else if (lexw_ns() == 2) HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<2>, 256, 0));
-        else HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<3>, 256, 0));
+        if (lexw_ns() == 1) HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<1, false>, 256, 0));
+        else if (lexw_ns() == 2) HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<2, false>, 256, 0));
+        else HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<3, false>, 256, 0));
         resident_lexw_waves = std::max(1, std::min(lps, 4)) * 4 * prop.multiProcessorCount;
+        // tuning: tiles per launch (fewer = taller bands, less halo recompute)
+        if (const char* e = std::getenv("CFD_LEXW_WAVES")) resident_lexw_waves = std::max(64, std::atoi(e));
       }
       if (const char* e = std::getenv("CFD_PAIR_EDGE_PCT")) pair_edge_pct = std::max(10, std::min(100, std::atoi(e)));
       resident_pair_waves = pps * 4 * prop.multiProcessorCount;
@@ -734,20 +736,48 @@ class Solver {
   }
 
   // ---- lexicographic order, multi-block (lexw.hpp) ----
+  int lexw_offset() const { return (P.nx + P.ny) / 2 + 192; }
   static int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
   // iterations whose residual every cell has contributed after launch m (H0 = 2 + 2NS m)
   int lexw_done(int m, int ns) const { return m < 0 ? 0 : floordiv(2 + 2 * ns * m + 2 * ns - 2 - P.nx - P.ny, 2) + 1; }
 
-  void launch_lexw(int ns, const PairPlan& pl, const Geo& g, const double* pin, double* pout, const double* f,
-                   const LexCtl& L, int H0, int K, int ka, int kb, bool replay) {
+  // steady: every cell active in every half-sweep of the launch and in the
+  // previous launch's last one (no activity masks: the leaner kernel)
+  void launch_lexw(int ns, bool steady, const PairPlan& pl, const Geo& g, const double* pin, double* pout,
+                   const double* f, const LexCtl& L, int H0, int K, int ka, int kb, bool replay, int waves) {
     const int fl = replay ? 4 : 0;
     const int ne = pl.ctiles >= 2 ? 2 : 1;
-    const int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
+    int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
+    int rth = 0, rthe = 0;
+    if (!steady) {
+      // ramp launch: tile only the rows it touches (lexw_rows), in bands sized
+      // so that the tiles fill the device once
+      std::vector<int> rows(pl.ctiles);
+      long long tot = 0;
+      for (int c = 0; c < pl.ctiles; ++c) {
+        int lo, hi;
+        lexw_rows(g, H0, K, ns, c, &lo, &hi);
+        rows[c] = std::max(0, hi - lo + 1);
+        tot += rows[c] * ((c == 0 || c == pl.ctiles - 1) ? 100 / std::max(1, pair_edge_pct) : 1);
+      }
+      const int ex = march_extra(ns);
+      rth = (int)std::min<long long>(96, std::max<long long>(1, (tot + waves - 1) / std::max(1, waves)));
+      rth = std::max(1, std::min(96, (rth + ex + 9) / 10 * 10 - ex));
+      rthe = std::max(1, std::min(rth, (rth + ex) * pair_edge_pct / 100 - ex));
+      ntiles = 0;
+      for (int c = 0; c < pl.ctiles; ++c) {
+        const int th = (c == 0 || c == pl.ctiles - 1) ? rthe : rth;
+        ntiles += (rows[c] + th - 1) / th;
+      }
+    }
     if (ntiles == 0) return;
     const dim3 grid((ntiles + 3) / 4);
-    if (ns == 1) poisson_lexw_kernel<1><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl);
-    else if (ns == 2) poisson_lexw_kernel<2><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl);
-    else poisson_lexw_kernel<3><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl);
+#define CFD_LEXW_LAUNCH(NS, R) \
+  poisson_lexw_kernel<NS, R><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl, rth, rthe)
+    if (ns == 1) { if (steady) CFD_LEXW_LAUNCH(1, false); else CFD_LEXW_LAUNCH(1, true); }
+    else if (ns == 2) { if (steady) CFD_LEXW_LAUNCH(2, false); else CFD_LEXW_LAUNCH(2, true); }
+    else { if (steady) CFD_LEXW_LAUNCH(3, false); else CFD_LEXW_LAUNCH(3, true); }
+#undef CFD_LEXW_LAUNCH
   }
 
   // K lexicographic iterations of every cell as launches m = 0.. (half-sweeps
@@ -759,14 +789,16 @@ class Solver {
     const int ns = lexw_ns();
     const int Hlast = P.nx + P.ny + 2 * (K - 1);
     const int nl = (Hlast - 2) / (2 * ns) + 1;  // last launch covers Hlast
-    const int kmax = P.max_iters + (P.nx + P.ny) / 2 + 64;
+    const int kmax = lexw_offset();
     LexCtl L{lexbits, (int)(lexbits_words / LEXW_SHARDS), kmax, tolv, stop};
     std::vector<PairPlan> plans(S.size());
     for (size_t q = 0; q < S.size(); ++q)
-      plans[q] = multi_plan(S[q].g.wj0, S[q].g.wj1 + 1, 0, 0, resident_lexw_waves / (int)S.size(), ns, 200);
-    // steady launches: every cell active in every half-sweep (H0 >= nx+ny, H0+2NS-1 <= 2K)
-    const int ms0 = (P.nx + P.ny - 2 + 2 * ns - 1) / (2 * ns), ms1 = (2 * K - 2 * ns + 1 - 2) / (2 * ns);
-    const bool steady = time_steady && ms1 >= ms0 && ms0 >= 0;
+      plans[q] = multi_plan(S[q].g.wj0, S[q].g.wj1 + 1, 0, 0, resident_lexw_waves / (int)S.size(), ns,
+                            96);  // (a wave's march <= 118 rows: its iterations fit one 64-bit mask)
+    // steady launches: every cell active in every half-sweep of the launch and
+    // of the previous one's last (nx+ny+1 <= H0 <= 2K-2NS+1, H0 = 2 + 2NS m)
+    const int ms0 = (P.nx + P.ny - 1 + 2 * ns - 1) / (2 * ns), ms1 = floordiv(2 * K - 2 * ns - 1, 2 * ns);
+    const bool steady = time_steady && ms1 >= ms0;
     const int chunk = P.chunk > 0 ? P.chunk : 32;
     int tested = tests ? -1 : K;  // highest iteration tested
     bool stopped = false;
@@ -788,8 +820,8 @@ class Solver {
         if (multi()) exchange(bin, HALO);
         if (steady && m == ms0) HIPC(hipEventRecord(ev_f0, st));
         for (size_t q = 0; q < S.size(); ++q)
-          launch_lexw(ns, plans[q], S[q].g, S[q].b[bin], S[q].b[bout], S[q].b[B_F], L, 2 + 2 * ns * m, K, ka, kb,
-                      !tests);
+          launch_lexw(ns, m >= ms0 && m <= ms1, plans[q], S[q].g, S[q].b[bin], S[q].b[bout], S[q].b[B_F], L,
+                      2 + 2 * ns * m, K, ka, kb, !tests, resident_lexw_waves / (int)S.size());
         check_launch("poisson_lexw");
         if (steady && m == ms1) HIPC(hipEventRecord(ev_f1, st));
       }
@@ -813,7 +845,7 @@ class Solver {
         HIPC(hipMemcpy(hb.data(), lexbits, lexbits_words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         const size_t wps = lexbits_words / LEXW_SHARDS;
         for (int k = std::max(tested + 1, 1); k <= K - 1; ++k) {
-          const int qb = kmax - k;
+          const int qb = kmax + k;
           unsigned long long w = 0;
           for (int sh = 0; sh < LEXW_SHARDS; ++sh) w |= hb[(size_t)sh * wps + (qb >> 6)];
           if (!((w >> (qb & 63)) & 1ull)) {
@@ -845,8 +877,9 @@ class Solver {
       for (int b : {0, 1}) HIPC(hipMemsetAsync(s.b[pbuf(b)], 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
     solve_tolerance();
     if (multi()) exchange(B_F, HALO - 1);
-    const int kmax = K + (P.nx + P.ny) / 2 + 64;
-    const size_t words = (size_t)LEXW_SHARDS * (kmax / 64 + 2);
+    // bit of iteration k: k + offset; waves touch iterations from about
+    // -(nx+ny)/2 (cells not yet started) to K + (nx+ny)/2 (cells finished)
+    const size_t words = (size_t)LEXW_SHARDS * ((lexw_offset() + K + (P.nx + P.ny) / 2 + 256) / 64 + 2);
     if (lexbits_words < words) {
       if (lexbits) HIPC(hipFree(lexbits));
       lexbits = nullptr;
