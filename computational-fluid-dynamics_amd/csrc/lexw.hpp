@@ -46,6 +46,17 @@ constexpr int LEXW_SHARDS = 8;
 #endif
 #define CFD_LEXW_MIN_WAVES(NS) ((NS) <= 2 ? CFD_LEXW_W2 : CFD_LEXW_W3)  // copies of the exceedance bitset (by block, ~XCD)
 
+// Ramp-launch tiling: bands of `th` rows from row `row0`; band b holds the
+// column tiles ca..cb (the ones its rows touch), numbered from first: band[b]
+// = first << 16 | ca << 8 | cb. Waves map to tiles band by band, column tiles
+// side by side (their shared halo columns are read together from one L2),
+// with no empty tiles (a workgroup holds its slot until its last wave ends).
+constexpr int LEXW_RAMP_BANDS = 256;
+struct LexRamp {
+  int nb, th, row0;
+  unsigned band[LEXW_RAMP_BANDS];
+};
+
 struct LexCtl {
   unsigned long long* bits;  // LEXW_SHARDS x words; bit q of the bitset <-> iteration q - kmax
   int words;                 // per shard
@@ -136,10 +147,27 @@ __device__ __forceinline__ double2 lx_ld(const WaveCtx<CAVITY>& x, const double*
 // MODE LX_ACT: per-cell activity masks (tiles on the ramps); 0: every cell
 // active in every half-sweep of the launch. Wall columns (the first and last
 // column tile, `edge`) take wave-uniform branches inside the same code.
+// Cell (j,i) is active in half-sweep H iff i+j <= H <= i+j+2(K-1). Every row
+// the march touches at front row R is j = R+X in half-sweep H0+h with h-X =
+// -1 (red at X = 2S+1 in H0+2S, black at 2S+2 in H0+2S+1), so with u = H0-1
+// -gi-R the update of column gi is active iff 0 <= u <= 2(K-1), of gi+1 iff
+// that holds for u-1, and the residual (half-sweep H-1) of gi / gi+1 for u-1
+// / u-2: three compares per march step, shared by all 2NS rows.
+// (LX_PIN: the masked values are pinned with an empty asm before their
+// selects; otherwise the compiler sinks the updates into exec-masked branches,
+// which split the march loop into dozens of blocks, serialise its loads and
+// ran the ramp launches at half the steady kernel's speed.)
 constexpr int LX_ACT = 1;
+struct LxAct {
+  bool a, b, c;  // u, u-1, u-2 within [0, 2(K-1)]
+};
 template <int MODE>
-__device__ __forceinline__ bool lx_active(const LexCtx& lc, int s, int H) {
-  return !(MODE & LX_ACT) || (s <= H && H <= s + 2 * (lc.K - 1));
+__device__ __forceinline__ LxAct lx_act(const LexCtx& lc, int gi, int R) {
+  if constexpr (!(MODE & LX_ACT)) return LxAct{true, true, true};
+  const unsigned span = 2u * (unsigned)(lc.K - 1);
+  unsigned u = (unsigned)(lc.H0 - 1 - R - gi);
+  asm volatile("" : "+v"(u));  // (opaque: no loop splitting on the induction variable R)
+  return LxAct{u <= span, u - 1u <= span, u - 2u <= span};
 }
 
 // SOR update (cavity-01.cpp:643-654). The solve's field starts at zero with
@@ -180,23 +208,23 @@ __device__ __forceinline__ double lx_res(const WaveCtx<CAVITY>& x, bool edge, in
 // ramp tiles, for cells outside the grid or inactive at H-1).
 template <int ROT, int JPAR, int COLOR, int MODE, bool STORE>
 __device__ __forceinline__ double lx_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool edge, double2 (&W)[5], int j,
-                                       int X, int H, const double2& fc) {
+                                       int X, const LxAct& act, const double2& fc) {
   double2& m = W[LX_SLOT(X)];
   const double2 nb = W[LX_SLOT(X + 1)], sb = W[LX_SLOT(X - 1)];  // rows j+1 (N), j-1 (S)
   const double2 old = m;
-  const bool upd = j > x.rmin && j < x.rmax;  // row-uniform
+  const bool upd = j > x.rmin && j < x.rmax;  // row-uniform (rows 1..ny: rmin/rmax exclude the ghost rows)
   // this colour's slot: a (even column gi) iff (j + COLOR) even
   constexpr bool A = ((JPAR ^ COLOR) & 1) == 0;
-  if (upd) {  // (rows 1..ny: rmin/rmax exclude the ghost rows)
-    if (A) {
-      const double Lb = dpp_from_left(m.y);
-      const double nv = lx_upd(x, lc, edge, j, x.gi, m.x, Lb, m.y, sb.x, nb.x, fc.x);
-      m.x = lx_active<MODE>(lc, x.gi + j, H) ? nv : m.x;
-    } else {
-      const double Ra = dpp_from_right(m.x);
-      const double nv = lx_upd(x, lc, edge, j, x.gi + 1, m.y, m.x, Ra, sb.y, nb.y, fc.y);
-      m.y = lx_active<MODE>(lc, x.gi + 1 + j, H) ? nv : m.y;
-    }
+  // (computed unconditionally and selected: branches on the row-uniform
+  // conditions split the march loop and serialise its loads)
+  {
+    const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
+    double nv = A ? lx_upd(x, lc, edge, j, x.gi, m.x, Lb, m.y, sb.x, nb.x, fc.x)
+                  : lx_upd(x, lc, edge, j, x.gi + 1, m.y, m.x, Ra, sb.y, nb.y, fc.y);
+    asm volatile("" : "+v"(nv));
+    const bool ok = upd && (!(MODE & LX_ACT) || (A ? act.a : act.b));
+    if (A) m.x = ok ? nv : m.x;
+    else m.y = ok ? nv : m.y;
   }
   if (STORE && j >= x.y0 && j < x.y1 && x.out_lane) {
     double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
@@ -204,8 +232,9 @@ __device__ __forceinline__ double lx_row(const WaveCtx<CAVITY>& x, const LexCtx&
     d2v mv = {m.x, m.y};
     __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
   }
-  // residual of the other colour's cell of this lane (iteration of half-sweep H-1)
-  if (!(j >= x.y0 && j < x.y1 && j >= x.g.j0 && j <= x.g.j1)) return 0.0;  // row-uniform
+  // residual of the other colour's cell of this lane (iteration of half-sweep
+  // H-1); 0 outside the wave's output rows
+  const bool rrow = j >= x.y0 && j < x.y1 && j >= x.g.j0 && j <= x.g.j1;  // row-uniform
   double r;
   int i;
   if (A) {  // updated: slot a (gi); the other colour is at gi+1: W = gi (old), E = gi+2 (lane l+1, new)
@@ -217,22 +246,23 @@ __device__ __forceinline__ double lx_row(const WaveCtx<CAVITY>& x, const LexCtx&
     const double Wv = dpp_from_left(old.y);
     r = lx_res(x, edge, j, i, m.x, Wv, m.y, sb.x, nb.x, fc.x);
   }
-  if (edge) r = (i >= 1 && i <= x.g.nx) ? r : 0.0;
-  if (MODE & LX_ACT) r = lx_active<MODE>(lc, i + j, H - 1) ? r : 0.0;
+  asm volatile("" : "+v"(r));
+  const bool rok = rrow && (!edge || (i >= 1 && i <= x.g.nx)) && (!(MODE & LX_ACT) || (A ? act.c : act.b));
+  r = rok ? r : 0.0;
   return r;
 }
 
 template <int S, int NS, int ROT, int PAR, int MODE>
 __device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool edge, LexRun<NS>& s, int R,
-                                          double& rs) {
+                                          const LxAct& act, double& rs) {
   if constexpr (S < NS) {
     // red at R+2S+1 (parity PAR^1) in half-sweep H0+2S; black at R+2S+2 (PAR) in H0+2S+1
-    rs = fmax(rs, lx_row<ROT, PAR ^ 1, 0, MODE, false>(x, lc, edge, s.w[S], R + 2 * S + 1, 2 * S + 1, lc.H0 + 2 * S,
+    rs = fmax(rs, lx_row<ROT, PAR ^ 1, 0, MODE, false>(x, lc, edge, s.w[S], R + 2 * S + 1, 2 * S + 1, act,
                                                        s.fr[LX_S10(2 * S + 1)]));
-    rs = fmax(rs, lx_row<ROT, PAR, 1, MODE, S == NS - 1>(x, lc, edge, s.w[S], R + 2 * S + 2, 2 * S + 2,
-                                                         lc.H0 + 2 * S + 1, s.fr[LX_S10(2 * S + 2)]));
+    rs = fmax(rs, lx_row<ROT, PAR, 1, MODE, S == NS - 1>(x, lc, edge, s.w[S], R + 2 * S + 2, 2 * S + 2, act,
+                                                         s.fr[LX_S10(2 * S + 2)]));
     if constexpr (S + 1 < NS) s.w[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
-    lx_sweeps<S + 1, NS, ROT, PAR, MODE>(x, lc, edge, s, R, rs);
+    lx_sweeps<S + 1, NS, ROT, PAR, MODE>(x, lc, edge, s, R, act, rs);
   }
 }
 
@@ -244,7 +274,8 @@ __device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& 
   s.np[LX_SLOT(-4)] = lx_ld(x, x.pin, R - 4);
   s.nf[LX_SLOT(-4)] = lx_ld(x, x.f, R - 3);
   double rs = 0.0;
-  lx_sweeps<0, NS, ROT, PAR, MODE>(x, lc, edge, s, R, rs);
+  const LxAct act = lx_act<MODE>(lc, x.gi, R);
+  lx_sweeps<0, NS, ROT, PAR, MODE>(x, lc, edge, s, R, act, rs);
   s.mask |= (rs > lc.tol) ? bit : 0ull;
 }
 
@@ -344,7 +375,7 @@ template <int NS, bool RAMP>
 __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisson_lexw_kernel(Geo g, Coef c, const double* __restrict__ pin,
                                                               double* __restrict__ pout, const double* __restrict__ f,
                                                               LexCtl L, int H0, int K, int ka, int kb, PairPlan pl,
-                                                              int flags, int rth, int rthe) {
+                                                              int flags, LexRamp rp) {
   constexpr int CH = 8;  // column halo (lanes 0-3 and 60-63)
   constexpr int H = 2 * NS + 1;
   const int lane = threadIdx.x & 63;
@@ -357,21 +388,21 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   const int blk = (bl < L8) ? (bl % 8) * (nblk / 8) + bl / 8 : bl;
   const int tile = blk * 4 + wv;
   int ctile, y0, y1;
-  if (rth > 0) {  // ramp launch: only the rows this launch touches, per column tile (lexw_rows)
-    int t = tile;
-    for (ctile = 0; ctile < pl.ctiles; ++ctile) {
-      int lo, hi;
-      lexw_rows(g, H0, K, NS, ctile, &lo, &hi);
-      const int th = (ctile == 0 || ctile == pl.ctiles - 1) ? rthe : rth;
-      const int nb = hi >= lo ? (hi - lo + th) / th : 0;
-      if (t < nb) {
-        y0 = lo + t * th;
-        y1 = min(y0 + th, hi + 1);
-        break;
-      }
-      t -= nb;
+  if (rp.nb > 0) {  // ramp launch (LexRamp): binary search of the tile's band
+    int lo = 0, hi = rp.nb - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if ((int)(rp.band[mid] >> 16) <= tile) lo = mid;
+      else hi = mid - 1;
     }
-    if (ctile >= pl.ctiles) return;
+    const unsigned e = rp.band[lo];
+    const int ca = (e >> 8) & 255, cb = e & 255;
+    ctile = ca + (tile - (int)(e >> 16));
+    if (ctile > cb) return;
+    int rlo, rhi;
+    lexw_rows(g, H0, K, NS, ctile, &rlo, &rhi);
+    y0 = max(rp.row0 + lo * rp.th, rlo);
+    y1 = min(rp.row0 + (lo + 1) * rp.th, rhi + 1);
   } else {
     const int ne = (pl.ctiles >= 2) ? 2 : 1;
     const int nbe = pl.nbe0 + pl.nbe1, nbi = pl.nb0 + pl.nb1;
@@ -423,10 +454,17 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   x.icol_b = gi + 1 >= 1 && gi + 1 <= g.nx;
   x.open_a = x.open_b = true;
   x.gic = min(max(gi, 0), g.pitch - 2);
-  LexCtx lc{H0, K, L.tol[0], c.om_nc[2], c.om_nc[3], c.om_nc[4]};
-  asm("" : "+s"(lc.o2), "+s"(lc.o3), "+s"(lc.o4));
+  // (readfirstlane: opaque wave-uniform values, so selects between them stay
+  // selects of values)
+  auto uni = [](double v) {
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+  };
+  LexCtx lc{H0, K, L.tol[0], uni(c.om_nc[2]), uni(c.om_nc[3]), uni(c.om_nc[4])};
   const int shard = bl & (LEXW_SHARDS - 1);
   const bool edge = !cols_in;
+  // (one march per kernel: an unmasked march inlined next to the masked one
+  // in the ramp kernel ran at half the steady kernel's speed)
   if constexpr (RAMP) lx_march<NS, LX_ACT>(x, lc, L, edge, y0, y1, c0, lane, shard);
   else lx_march<NS, 0>(x, lc, L, edge, y0, y1, c0, lane, shard);
 }

@@ -748,32 +748,58 @@ class Solver {
     const int fl = replay ? 4 : 0;
     const int ne = pl.ctiles >= 2 ? 2 : 1;
     int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
-    int rth = 0, rthe = 0;
-    if (!steady) {
-      // ramp launch: tile only the rows it touches (lexw_rows), in bands sized
-      // so that the tiles fill the device once
-      std::vector<int> rows(pl.ctiles);
+    LexRamp rp{};
+    static const bool ramp_all = std::getenv("CFD_LEXW_RAMP_TILING") != nullptr;  // diagnostic
+    if (!steady || ramp_all) {
+      // ramp launch: tile only the rows it touches (lexw_rows), bands of the
+      // shortest height whose tiles fit one resident round, at most the
+      // steady plan's (at that every ramp launch fits: it touches fewer rows)
+      int rl = 1 << 30, rh = -1;
       long long tot = 0;
+      std::vector<std::pair<int, int>> rr(pl.ctiles);
       for (int c = 0; c < pl.ctiles; ++c) {
-        int lo, hi;
-        lexw_rows(g, H0, K, ns, c, &lo, &hi);
-        rows[c] = std::max(0, hi - lo + 1);
-        tot += rows[c] * ((c == 0 || c == pl.ctiles - 1) ? 100 / std::max(1, pair_edge_pct) : 1);
+        lexw_rows(g, H0, K, ns, c, &rr[c].first, &rr[c].second);
+        if (rr[c].second >= rr[c].first) {
+          rl = std::min(rl, rr[c].first);
+          rh = std::max(rh, rr[c].second);
+          tot += rr[c].second - rr[c].first + 1;
+        }
       }
+      if (rh < rl) return;
       const int ex = march_extra(ns);
-      rth = (int)std::min<long long>(96, std::max<long long>(1, (tot + waves - 1) / std::max(1, waves)));
-      rth = std::max(1, std::min(96, (rth + ex + 9) / 10 * 10 - ex));
-      rthe = std::max(1, std::min(rth, (rth + ex) * pair_edge_pct / 100 - ex));
-      ntiles = 0;
-      for (int c = 0; c < pl.ctiles; ++c) {
-        const int th = (c == 0 || c == pl.ctiles - 1) ? rthe : rth;
-        ntiles += (rows[c] + th - 1) / th;
-      }
-    }
-    if (ntiles == 0) return;
+      auto build = [&](int th) {  // fills rp for band height th; returns the tile count
+        rp.th = th;
+        rp.row0 = rl;
+        rp.nb = (rh - rl) / th + 1;
+        int n = 0;
+        for (int b = 0; b < rp.nb; ++b) {
+          const int blo = rl + b * th, bhi = blo + th - 1;
+          int ca = -1, cb = -2;
+          for (int c = 0; c < pl.ctiles; ++c)
+            if (std::max(blo, rr[c].first) <= std::min(bhi, rr[c].second)) {
+              if (ca < 0) ca = c;
+              cb = c;
+            }
+          if (ca < 0) ca = 0, cb = -1;  // (an empty band: no tiles)
+          rp.band[b] = ((unsigned)n << 16) | ((unsigned)ca << 8) | (unsigned)(cb < 0 ? 0 : cb);
+          if (cb < 0) rp.band[b] = ((unsigned)n << 16) | 1u << 8;  // ca 1 > cb 0: empty
+          n += std::max(0, cb - ca + 1);
+        }
+        return n;
+      };
+      int th = (int)std::max<long long>(1, (tot + waves - 1) / std::max(1, waves));
+      th = std::max(1, (th + ex + 9) / 10 * 10 - ex);
+      while ((rh - rl) / th + 1 > LEXW_RAMP_BANDS) th += 10;
+      ntiles = build(th);
+      while (th < pl.th && ntiles > waves) ntiles = build(th += 10);
+      if (th > pl.th) ntiles = build(th = std::max(pl.th, (rh - rl) / LEXW_RAMP_BANDS + 1));
+      if (pl.ctiles > 255 || ntiles >= 65536) throw Error(CFD_E_ARG, "lexicographic ordering: grid too wide");
+    }    if (ntiles == 0) return;
     const dim3 grid((ntiles + 3) / 4);
 #define CFD_LEXW_LAUNCH(NS, R) \
-  poisson_lexw_kernel<NS, R><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl, rth, rthe)
+  poisson_lexw_kernel<NS, R><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl, rp)
+    static const bool all_ramp_kernel = std::getenv("CFD_LEXW_RAMP_KERNEL") != nullptr;  // diagnostic
+    if (all_ramp_kernel) steady = false;
     if (ns == 1) { if (steady) CFD_LEXW_LAUNCH(1, false); else CFD_LEXW_LAUNCH(1, true); }
     else if (ns == 2) { if (steady) CFD_LEXW_LAUNCH(2, false); else CFD_LEXW_LAUNCH(2, true); }
     else { if (steady) CFD_LEXW_LAUNCH(3, false); else CFD_LEXW_LAUNCH(3, true); }
