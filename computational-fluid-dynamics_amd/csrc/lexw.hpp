@@ -170,61 +170,75 @@ __device__ __forceinline__ LxAct lx_act(const LexCtx& lc, int gi, int R) {
   return LxAct{u <= span, u - 1u <= span, u - 2u <= span};
 }
 
-// SOR update (cavity-01.cpp:643-654). The solve's field starts at zero with
-// +0.0 ghosts that never change, so a wall's indicator product 0*p_ghost is
-// +0.0 = p_ghost itself: only omega/nc differs at the walls (nc = 4 - walls
-// among W, E, N; es = 1 always). Row-uniform j == ny, lane-constant wall.
-// Ghost / outside columns of an edge tile are not updated: omega/nc = 0 and
-// 1 - omega = 1 there give pc + 0*(finite) = pc (+0.0 ghosts stay +0.0).
-__device__ __forceinline__ double lx_upd(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool edge, int j, int i,
-                                         double pc, double pW, double pE, double pS, double pN, double fc) {
-  const Coef& c = x.c;
-  const double sum = (pE + pW) + (pN + pS) - fc * c.h2;
-  const bool top = j == x.g.ny;  // row-uniform
-  if (!edge) return pc * c.one_m_omega + (top ? lc.o3 : lc.o4) * sum;
+// SOR update (cavity-01.cpp:643-654) as pc*omm + om*sum in every cell. The
+// solve's field starts at zero with +0.0 ghosts that never change, so a wall's
+// indicator product 0*p_ghost is +0.0 = p_ghost itself: only omega/nc differs
+// at the walls (nc = 4 - walls among W, E, N; es = 1 always). A cell that is
+// not updated (ghost rows and columns, rows outside the stored strip) takes om
+// = 0, omm = 1: pc*1 + 0*sum = pc for finite sum and pc != -0.0 (the field is
+// never -0.0: a sum is -0.0 only when both terms are). Interior tiles choose
+// om / omm per row (row-uniform: scalar selects, no vector work); wall tiles
+// (EDGE) per lane from values fixed for the wave (LxCol).
+struct LxCol {
+  int k;  // column kind: 0 outside the grid, 1 wall (i = 1 or nx), 2 interior
+};
+__device__ __forceinline__ LxCol lx_col(const WaveCtx<CAVITY>& x, int i) {
   const bool in = i >= 1 && i <= x.g.nx;
   const bool wall = (i == 1) || (i == x.g.nx);
-  const double omw = top ? lc.o2 : lc.o3, omi = top ? lc.o3 : lc.o4;
-  const double om = !in ? 0.0 : wall ? omw : omi;
-  const double omm = in ? c.one_m_omega : 1.0;
+  return LxCol{!in ? 0 : wall ? 1 : 2};
+}
+template <bool EDGE>
+__device__ __forceinline__ double lx_upd(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool upd, bool top,
+                                         const LxCol& cc, double pc, double pW, double pE, double pS, double pN,
+                                         double fc) {
+  const double sum = (pE + pW) + (pN + pS) - fc * x.c.h2;
+  const double oi = upd ? (top ? lc.o3 : lc.o4) : 0.0;  // row-uniform
+  double om, omm;
+  if constexpr (EDGE) {  // (a kind per lane, not per-lane coefficients: registers)
+    const double ow = upd ? (top ? lc.o2 : lc.o3) : 0.0;
+    om = cc.k == 2 ? oi : cc.k == 1 ? ow : 0.0;
+    omm = (upd && cc.k != 0) ? x.c.one_m_omega : 1.0;
+  } else {
+    om = oi;
+    omm = upd ? x.c.one_m_omega : 1.0;
+  }
   return pc * omm + om * sum;
 }
 
-// |residual| (cavity-01.cpp:659-677) with the indicator products as selects
-// (residual_abs): the same |r| bits.
-__device__ __forceinline__ double lx_res(const WaveCtx<CAVITY>& x, bool edge, int j, int i, double pc, double pW,
-                                         double pE, double pS, double pN, double fc) {
-  if (!edge && j != x.g.ny) return residual_interior<CAVITY>(x.c, pc, pW, pE, pS, pN, fc);
-  const double tE = (!edge || i < x.g.nx) ? (pE - pc) : 0.0;
-  const double tW = (!edge || i > 1) ? (pW - pc) : 0.0;
-  const double tN = (j < x.g.ny) ? (pN - pc) : 0.0;
-  const double tS = pS - pc;
-  return fabs(x.c.idx2 * (tE + tW + tN + tS) - fc);
+// |residual| (cavity-01.cpp:659-677) in residual_interior's order with the
+// north term scaled by eN (0 in the top row, 1 below): (pN-pc)*1 is exact and
+// the sign of a zero term cannot change |r|. Wall tiles (EDGE) take
+// residual_abs's selects for the east / west terms.
+template <bool EDGE>
+__device__ __forceinline__ double lx_res(const WaveCtx<CAVITY>& x, double eN, int i, double pc, double pW, double pE,
+                                         double pS, double pN, double fc) {
+  const double tE = (!EDGE || i < x.g.nx) ? (pE - pc) : 0.0;
+  const double tW = (!EDGE || i > 1) ? (pW - pc) : 0.0;
+  return fabs(x.c.idx2 * (tE + tW + (pN - pc) * eN + (pS - pc)) - fc);
 }
 
-// Update of row j = R + X (colour COLOR at half-sweep H) and, from the old and
-// new values, |residual| of the other colour's cell of this lane (iteration of
-// half-sweep H-1; 0 for rows outside the wave's output rows and, in edge /
-// ramp tiles, for cells outside the grid or inactive at H-1).
-template <int ROT, int JPAR, int COLOR, int MODE, bool STORE>
-__device__ __forceinline__ double lx_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool edge, double2 (&W)[5], int j,
-                                       int X, const LxAct& act, const double2& fc) {
+// Update of row j = R + X (colour COLOR) and, from the old and new values, the
+// test |residual| > tol of the other colour's cell of this lane (iteration of
+// half-sweep H-1; false for rows outside the wave's output rows and, in edge /
+// ramp tiles, for cells outside the grid or inactive at H-1). Straight-line
+// code: branches on the row-uniform conditions split the march loop and
+// serialise its loads, so they become scalar coefficients and thresholds.
+template <int ROT, int JPAR, int COLOR, int MODE, bool EDGE, bool STORE>
+__device__ __forceinline__ void lx_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCol (&cc)[2],
+                                       double2 (&W)[5], int j, int X, const LxAct& act, const double2& fc, int& exi) {
   double2& m = W[LX_SLOT(X)];
   const double2 nb = W[LX_SLOT(X + 1)], sb = W[LX_SLOT(X - 1)];  // rows j+1 (N), j-1 (S)
   const double2 old = m;
   const bool upd = j > x.rmin && j < x.rmax;  // row-uniform (rows 1..ny: rmin/rmax exclude the ghost rows)
+  const bool top = j == x.g.ny;
   // this colour's slot: a (even column gi) iff (j + COLOR) even
   constexpr bool A = ((JPAR ^ COLOR) & 1) == 0;
-  // (computed unconditionally and selected: branches on the row-uniform
-  // conditions split the march loop and serialise its loads)
-  {
-    const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
-    double nv = A ? lx_upd(x, lc, edge, j, x.gi, m.x, Lb, m.y, sb.x, nb.x, fc.x)
-                  : lx_upd(x, lc, edge, j, x.gi + 1, m.y, m.x, Ra, sb.y, nb.y, fc.y);
-    asm volatile("" : "+v"(nv));
-    const bool ok = upd && (!(MODE & LX_ACT) || (A ? act.a : act.b));
-    if (A) m.x = ok ? nv : m.x;
-    else m.y = ok ? nv : m.y;
+  if constexpr (A) {
+    double nv = lx_upd<EDGE>(x, lc, upd, top, cc[0], m.x, dpp_from_left(m.y), m.y, sb.x, nb.x, fc.x);
+    m.x = ((MODE & LX_ACT) && !act.a) ? m.x : nv;
+  } else {
+    double nv = lx_upd<EDGE>(x, lc, upd, top, cc[1], m.y, m.x, dpp_from_right(m.x), sb.y, nb.y, fc.y);
+    m.y = ((MODE & LX_ACT) && !act.b) ? m.y : nv;
   }
   if (STORE && j >= x.y0 && j < x.y1 && x.out_lane) {
     double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
@@ -233,50 +247,51 @@ __device__ __forceinline__ double lx_row(const WaveCtx<CAVITY>& x, const LexCtx&
     __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
   }
   // residual of the other colour's cell of this lane (iteration of half-sweep
-  // H-1); 0 outside the wave's output rows
+  // H-1), tested against +inf outside the wave's output rows
   const bool rrow = j >= x.y0 && j < x.y1 && j >= x.g.j0 && j <= x.g.j1;  // row-uniform
-  double r;
-  int i;
-  if (A) {  // updated: slot a (gi); the other colour is at gi+1: W = gi (old), E = gi+2 (lane l+1, new)
-    i = x.gi + 1;
-    const double E = dpp_from_right(m.x);
-    r = lx_res(x, edge, j, i, m.y, old.x, E, sb.y, nb.y, fc.y);
+  const double thr = rrow ? lc.tol : __builtin_huge_val();
+  const double eN = top ? 0.0 : 1.0;
+  bool ex;
+  if constexpr (A) {  // updated: slot a (gi); the other colour is at gi+1: W = gi (old), E = gi+2 (lane l+1, new)
+    ex = lx_res<EDGE>(x, eN, x.gi + 1, m.y, old.x, dpp_from_right(m.x), sb.y, nb.y, fc.y) > thr;
+    if constexpr (EDGE) ex = ex && x.icol_b;
+    if constexpr ((MODE & LX_ACT) != 0) ex = ex && act.c;
   } else {  // updated: slot b (gi+1); the other colour is at gi: W = gi-1 (lane l-1, old), E = gi+1 (new)
-    i = x.gi;
-    const double Wv = dpp_from_left(old.y);
-    r = lx_res(x, edge, j, i, m.x, Wv, m.y, sb.x, nb.x, fc.x);
+    ex = lx_res<EDGE>(x, eN, x.gi, m.x, dpp_from_left(old.y), m.y, sb.x, nb.x, fc.x) > thr;
+    if constexpr (EDGE) ex = ex && x.icol_a;
+    if constexpr ((MODE & LX_ACT) != 0) ex = ex && act.b;
   }
-  asm volatile("" : "+v"(r));
-  const bool rok = rrow && (!edge || (i >= 1 && i <= x.g.nx)) && (!(MODE & LX_ACT) || (A ? act.c : act.b));
-  r = rok ? r : 0.0;
-  return r;
+  // (an int flag per lane, pinned row by row: a test deferred by the
+  // scheduler keeps its residual live, dozens of them across the loop)
+  exi = ex ? 1 : exi;
+  asm volatile("" : "+v"(exi));
 }
 
-template <int S, int NS, int ROT, int PAR, int MODE>
-__device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool edge, LexRun<NS>& s, int R,
-                                          const LxAct& act, double& rs) {
+template <int S, int NS, int ROT, int PAR, int MODE, bool EDGE>
+__device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCol (&cc)[2],
+                                          LexRun<NS>& s, int R, const LxAct& act, int& exi) {
   if constexpr (S < NS) {
     // red at R+2S+1 (parity PAR^1) in half-sweep H0+2S; black at R+2S+2 (PAR) in H0+2S+1
-    rs = fmax(rs, lx_row<ROT, PAR ^ 1, 0, MODE, false>(x, lc, edge, s.w[S], R + 2 * S + 1, 2 * S + 1, act,
-                                                       s.fr[LX_S10(2 * S + 1)]));
-    rs = fmax(rs, lx_row<ROT, PAR, 1, MODE, S == NS - 1>(x, lc, edge, s.w[S], R + 2 * S + 2, 2 * S + 2, act,
-                                                         s.fr[LX_S10(2 * S + 2)]));
+    lx_row<ROT, PAR ^ 1, 0, MODE, EDGE, false>(x, lc, cc, s.w[S], R + 2 * S + 1, 2 * S + 1, act,
+                                               s.fr[LX_S10(2 * S + 1)], exi);
+    lx_row<ROT, PAR, 1, MODE, EDGE, S == NS - 1>(x, lc, cc, s.w[S], R + 2 * S + 2, 2 * S + 2, act,
+                                                 s.fr[LX_S10(2 * S + 2)], exi);
     if constexpr (S + 1 < NS) s.w[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
-    lx_sweeps<S + 1, NS, ROT, PAR, MODE>(x, lc, edge, s, R, act, rs);
+    lx_sweeps<S + 1, NS, ROT, PAR, MODE, EDGE>(x, lc, cc, s, R, act, exi);
   }
 }
 
-template <int NS, int ROT, int PAR, int MODE>  // PAR = parity of R
-__device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& lc, bool edge, LexRun<NS>& s, int R,
-                                        unsigned long long bit) {
+template <int NS, int ROT, int PAR, int MODE, bool EDGE>  // PAR = parity of R
+__device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCol (&cc)[2],
+                                        LexRun<NS>& s, int R, unsigned long long bit) {
   s.w[0][LX_SLOT(0)] = s.np[LX_SLOT(0)];
   s.fr[LX_S10(1)] = s.nf[LX_SLOT(0)];
   s.np[LX_SLOT(-4)] = lx_ld(x, x.pin, R - 4);
   s.nf[LX_SLOT(-4)] = lx_ld(x, x.f, R - 3);
-  double rs = 0.0;
+  int exi = 0;
   const LxAct act = lx_act<MODE>(lc, x.gi, R);
-  lx_sweeps<0, NS, ROT, PAR, MODE>(x, lc, edge, s, R, act, rs);
-  s.mask |= (rs > lc.tol) ? bit : 0ull;
+  lx_sweeps<0, NS, ROT, PAR, MODE, EDGE>(x, lc, cc, s, R, act, exi);
+  s.mask |= exi ? bit : 0ull;
 }
 
 // OR across the wave's 64 lanes
@@ -303,9 +318,9 @@ __device__ __forceinline__ void lexw_flush(const LexCtl& L, int sh, int q0, cons
   }
 }
 
-template <int NS, int MODE>
-__device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L, bool edge, int y0,
-                                         int y1, int c0, int lane, int shard) {
+template <int NS, int MODE, bool EDGE>
+__device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L, int y0, int y1,
+                                         int c0, int lane, int shard) {
   constexpr int H = 2 * NS + 1;
   const int Rb0 = y1 - 1 + H;
   const int Rbeg = Rb0 + (Rb0 & 1);  // even first front row: compile-time colours
@@ -327,20 +342,22 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
     }
   }
   s.mask = 0ull;
+  LxCol cc[2];
+  if constexpr (EDGE) cc[0] = lx_col(x, x.gi), cc[1] = lx_col(x, x.gi + 1);
   int R = Rbeg;
   // (nsteps + 9 <= 127 by the host's band limit: bits t/2 < 64)
 #define LX_BIT(T) ((((st + (T)) >> 1) < 64) ? (1ull << ((st + (T)) >> 1)) : 0ull)
   for (int st = 0; st < nsteps; st += 10, R -= 10) {
-    lx_step<NS, 0, 0, MODE>(x, lc, edge, s, R, LX_BIT(0));
-    lx_step<NS, 1, 1, MODE>(x, lc, edge, s, R - 1, LX_BIT(1));
-    lx_step<NS, 2, 0, MODE>(x, lc, edge, s, R - 2, LX_BIT(2));
-    lx_step<NS, 3, 1, MODE>(x, lc, edge, s, R - 3, LX_BIT(3));
-    lx_step<NS, 4, 0, MODE>(x, lc, edge, s, R - 4, LX_BIT(4));
-    lx_step<NS, 0, 1, MODE>(x, lc, edge, s, R - 5, LX_BIT(5));
-    lx_step<NS, 1, 0, MODE>(x, lc, edge, s, R - 6, LX_BIT(6));
-    lx_step<NS, 2, 1, MODE>(x, lc, edge, s, R - 7, LX_BIT(7));
-    lx_step<NS, 3, 0, MODE>(x, lc, edge, s, R - 8, LX_BIT(8));
-    lx_step<NS, 4, 1, MODE>(x, lc, edge, s, R - 9, LX_BIT(9));
+    lx_step<NS, 0, 0, MODE, EDGE>(x, lc, cc, s, R, LX_BIT(0));
+    lx_step<NS, 1, 1, MODE, EDGE>(x, lc, cc, s, R - 1, LX_BIT(1));
+    lx_step<NS, 2, 0, MODE, EDGE>(x, lc, cc, s, R - 2, LX_BIT(2));
+    lx_step<NS, 3, 1, MODE, EDGE>(x, lc, cc, s, R - 3, LX_BIT(3));
+    lx_step<NS, 4, 0, MODE, EDGE>(x, lc, cc, s, R - 4, LX_BIT(4));
+    lx_step<NS, 0, 1, MODE, EDGE>(x, lc, cc, s, R - 5, LX_BIT(5));
+    lx_step<NS, 1, 0, MODE, EDGE>(x, lc, cc, s, R - 6, LX_BIT(6));
+    lx_step<NS, 2, 1, MODE, EDGE>(x, lc, cc, s, R - 7, LX_BIT(7));
+    lx_step<NS, 3, 0, MODE, EDGE>(x, lc, cc, s, R - 8, LX_BIT(8));
+    lx_step<NS, 4, 1, MODE, EDGE>(x, lc, cc, s, R - 9, LX_BIT(9));
   }
 #undef LX_BIT
   // lane l's bit u <-> iteration Bd0 + u - l = (Bd0 - 63) + (u + 63 - l):
@@ -463,10 +480,17 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   LexCtx lc{H0, K, L.tol[0], uni(c.om_nc[2]), uni(c.om_nc[3]), uni(c.om_nc[4])};
   const int shard = bl & (LEXW_SHARDS - 1);
   const bool edge = !cols_in;
-  // (one march per kernel: an unmasked march inlined next to the masked one
-  // in the ramp kernel ran at half the steady kernel's speed)
-  if constexpr (RAMP) lx_march<NS, LX_ACT>(x, lc, L, edge, y0, y1, c0, lane, shard);
-  else lx_march<NS, 0>(x, lc, L, edge, y0, y1, c0, lane, shard);
+  if constexpr (RAMP) {
+    // tiles of a ramp launch whose every cell is active in every half-sweep
+    // it evaluates (H0-1 .. H0+2NS-1) take the unmasked march
+    const bool full = smax <= H0 - 2 && Hend <= smin + last;
+    if (edge) lx_march<NS, LX_ACT, true>(x, lc, L, y0, y1, c0, lane, shard);
+    else if (full) lx_march<NS, 0, false>(x, lc, L, y0, y1, c0, lane, shard);
+    else lx_march<NS, LX_ACT, false>(x, lc, L, y0, y1, c0, lane, shard);
+  } else {
+    if (edge) lx_march<NS, 0, true>(x, lc, L, y0, y1, c0, lane, shard);
+    else lx_march<NS, 0, false>(x, lc, L, y0, y1, c0, lane, shard);
+  }
 }
 
 #undef LX_SLOT

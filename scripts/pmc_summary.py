@@ -1,66 +1,28 @@
 #!/usr/bin/env python3
-"""HBM traffic per launch of the SOR kernel from the two rocprofv3 PMC passes
-written by scripts/profile_round.sh (FETCH_SIZE and WRITE_SIZE, one pass each).
-
-Corrections (MI355X_MICROARCH.md, section "HBM [CDNA4]"): on gfx950 FETCH_SIZE
-reports exactly half of the bytes of a 16-B-per-lane streaming read, so it is
-doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores. Counter units
-are KiB per dispatch (summed over the XCDs by rocprofv3).
-
-usage: pmc_summary.py <pmc_dir> <kernel-substring> <out.json> [sweeps_per_launch]
-"""
-from __future__ import annotations
-
+"""Mean SQ counters of the lexw launches in a window of dispatches (steady
+phase by default) from a rocprofv3 counter_collection.csv."""
+import collections
 import csv
-import json
-import os
 import sys
 
-NX = 4096
-ROWS = 4098  # 4096 interior rows + 2 ghost rows (one strip)
-
-
-def mean_counter(path: str, kernel: str, counter: str) -> tuple[float, int]:
-    vals = []
-    with open(path) as fh:
-        for row in csv.DictReader(fh):
-            if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
-                vals.append(float(row["Counter_Value"]))
-    if not vals:
-        raise SystemExit(f"no {counter} samples for {kernel!r} in {path}")
-    return sum(vals) / len(vals), len(vals)
-
-
-def main() -> None:
-    d, kernel, out = sys.argv[1], sys.argv[2], sys.argv[3]
-    spl = int(sys.argv[4]) if len(sys.argv) > 4 else 2
-    f_kib, nf = mean_counter(os.path.join(d, "FETCH_SIZE", "run_counter_collection.csv"), kernel, "FETCH_SIZE")
-    w_kib, nw = mean_counter(os.path.join(d, "WRITE_SIZE", "run_counter_collection.csv"), kernel, "WRITE_SIZE")
-    rd = 2.0 * f_kib * 1024.0
-    wr = w_kib * 1024.0
-    algo = 24 * ROWS * (NX + 2)
-    res = {
-        "kernel": kernel,
-        "nx": NX,
-        "rows": ROWS,
-        "sweeps_per_launch": spl,
-        "dispatches": [nf, nw],
-        "FETCH_SIZE_KiB_raw": f_kib,
-        "WRITE_SIZE_KiB_raw": w_kib,
-        "correction": "FETCH_SIZE x2 (gfx950 reports half of 16-B/lane streaming reads), WRITE_SIZE as is "
-                      "(exact for 16-B/lane stores): MI355X_MICROARCH.md, HBM [CDNA4]",
-        "hbm_read_bytes_per_launch": rd,
-        "hbm_write_bytes_per_launch": wr,
-        "hbm_bytes_per_launch": rd + wr,
-        "algorithmic_bytes_per_launch": algo,
-        "traffic_over_algorithmic": (rd + wr) / algo,
-        "command": "rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE (separate passes) -- python3 bench.py --steps 1 "
-                   "--warmup 0 --max-iters 100 --no-cpu-baseline",
-    }
-    with open(out, "w") as fh:
-        json.dump(res, fh, indent=1)
-    print(json.dumps(res, indent=1))
-
-
-if __name__ == "__main__":
-    main()
+path = sys.argv[1]
+kind = sys.argv[2] if len(sys.argv) > 2 else "false"  # steady kernel
+d = collections.OrderedDict()
+for r in csv.DictReader(open(path)):
+    if "lexw" not in r["Kernel_Name"]:
+        continue
+    e = d.setdefault(r["Dispatch_Id"], {"k": "false" if "false>" in r["Kernel_Name"] else "true",
+                                        "vgpr": r["VGPR_Count"], "sgpr": r["SGPR_Count"]})
+    e[r["Counter_Name"]] = float(r["Counter_Value"])
+sel = [e for e in d.values() if e["k"] == kind]
+sel = sel[len(sel) // 4: 3 * len(sel) // 4] or sel
+agg = collections.Counter()
+for e in sel:
+    for k, v in e.items():
+        if k.startswith(("SQ_", "TCC_", "TCP_", "TA_", "GRBM_")):
+            agg[k] += v / len(sel)
+print(f"{len(sel)} dispatches of kernel<.., {kind}>  vgpr {sel[0]['vgpr']} sgpr {sel[0]['sgpr']}")
+for k, v in sorted(agg.items()):
+    print(f"  {k:24s} {v:16.0f}")
+if "SQ_INSTS_VALU" in agg and "SQ_WAVES" in agg:
+    print("  VALU per wave", agg["SQ_INSTS_VALU"] / agg["SQ_WAVES"], " SALU per wave", agg.get("SQ_INSTS_SALU", 0) / agg["SQ_WAVES"])
