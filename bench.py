@@ -15,7 +15,10 @@ sweeps per launch for the cavity: HIP events on the solver's stream over the
 timed region; `achieved` = the 24 B/cell one launch must move / launch time,
 `effective_sweep_*` the same per sweep), cpu_baseline (the oracle's
 lexicographic SOR loop — the reference's loop restated in C — on a bounded
-sample of the same grid, rank 0 only).
+sample of the same grid, rank 0 only), reference_order (N=1: the same
+workload in the reference's lexicographic sweep order, poisson_lexw_kernel,
+bit-identical to the reference's loop; the red-black order of the headline is
+bit-identical to the red-black oracle, and is what splits over GPUs).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--global-ny NY]
 For N > 1 launch with torch.distributed.run (one rank per GPU); halos and the
@@ -77,6 +80,41 @@ def cpu_baseline(nx: int, ny: int, budget_s: float, case: str = "cavity") -> dic
                       f"{nx}x{ny} {case} after one predictor step, {el:.1f} s single-threaded"}
 
 
+def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch: int) -> dict:
+    """The same workload in the reference's lexicographic sweep order
+    (ordering="lex": poisson_lexw_kernel, bit-identical to the reference's
+    loop at any size), timed the same way on one GPU: value, ms per step and
+    the steady launches' roofline (every cell active; the ramps at both ends of
+    a solve touch part of the grid)."""
+    import torch
+
+    s = C.solver_for(cp, device=device, check_every=check_every, ordering="lex",
+                     sweeps_per_launch=args.sweeps_per_launch or 3)
+    if args.case == "cavity":
+        s.applyBoundaryConditions()
+    s.step()  # warmup
+    s.synchronize()
+    s.reset_timing()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    iters = [s.step()[0] for _ in range(args.lex_steps)]
+    s.synchronize()
+    el = time.perf_counter() - t0
+    tm = s.timing()
+    s.close()
+    steady_ms = tm.poisson_steady_ms / max(tm.poisson_steady_launches, 1)
+    achieved = BYTES_PER_CELL * cells_per_launch / (steady_ms * 1e-3) / 1e9 if tm.poisson_steady_launches else None
+    return {"ordering": "lex", "value": round(tm.poisson_cell_updates / el / 1e6, 2), "unit": "MLUPS",
+            "ms_per_step": round(el / args.lex_steps * 1e3, 3), "steps": args.lex_steps,
+            "sor_iterations_per_step": iters,
+            "kernel": f"poisson_lexw_kernel<{args.sweeps_per_launch or 3}>",
+            "launches_per_step": round(tm.poisson_launches / args.lex_steps, 1),
+            "steady_launches_per_step": round(tm.poisson_steady_launches / args.lex_steps, 1),
+            "steady_launch_us": round(steady_ms * 1e3, 2) if tm.poisson_steady_launches else None,
+            "steady_achieved_GBs": round(achieved, 1) if achieved else None,
+            "steady_frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None}
+
+
 def kcase_of(case: str) -> str:
     return "cavity" if case == "rayleigh_benard" else case  # Rayleigh-Benard runs the cavity SOR kernels
 
@@ -101,6 +139,9 @@ def main() -> int:
                     help="red-black SOR iterations fused per kernel launch (0: auto = 3 for the cavity)")
     ap.add_argument("--ordering", default="rb", choices=["rb", "lex"],
                     help="SOR sweep order: rb (red-black) or lex (the reference's lexicographic order, bit-identical)")
+    ap.add_argument("--lex-steps", type=int, default=2,
+                    help="N=1 cavity: also time this many steps in the reference's own (lexicographic) order "
+                         "(0: skip); reported as reference_order")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -255,6 +296,10 @@ def main() -> int:
         if not args.no_cpu_baseline and world == 1:  # the CPU leg is timed at N=1 only
             log("timing the CPU baseline ...")
             line["cpu_baseline"] = cpu_baseline(cp.nx, cp.ny, args.cpu_seconds, args.case)
+
+    if rank == 0 and world == 1 and args.lex_steps > 0 and args.ordering == "rb" and kcase_of(args.case) == "cavity":
+        line["reference_order"] = reference_order(C, cp, args, local_rank, check_every, cells_per_launch)
+    if rank == 0:
         print(json.dumps(line), flush=True)
 
     solver.close()

@@ -9,7 +9,7 @@ path = sys.argv[1]
 kind = sys.argv[2] if len(sys.argv) > 2 else "false"  # steady kernel
 d = collections.OrderedDict()
 for r in csv.DictReader(open(path)):
-    if "lexw" not in r["Kernel_Name"]:
+    if (sys.argv[3] if len(sys.argv) > 3 else "lexw") not in r["Kernel_Name"]:
         continue
     e = d.setdefault(r["Dispatch_Id"], {"k": "false" if "false>" in r["Kernel_Name"] else "true",
                                         "vgpr": r["VGPR_Count"], "sgpr": r["SGPR_Count"]})
