@@ -47,6 +47,7 @@ struct Coef {
   double om_nc[5];         // cavity: omega / neighbour_count for counts 0..4
   double h2;               // cavity: grid_spacing * grid_spacing
   double denom;            // open cases: 2*(idx2+idy2)
+  double rdenom;           // open cases: 1.0 / denom (correctly rounded, host)
   double cav_src;          // cavity: (1/dt) * rho           (cavity-01.cpp:624)
   double open_src;         // open:   rho / dt               (channel-01.cpp:610)
   double cav_corr;         // cavity: (dt/h) * rho           (cavity-01.cpp:696,701)
@@ -397,6 +398,23 @@ __global__ void tol_kernel(Coef c, const double* __restrict__ srcmax, double* __
 // Ghost / solid refresh after each sweep: channel-01.cpp:531-541,
 // backwards_step-01.cpp:685-740.
 
+// x / denom, correctly rounded, without the divide sequence: q0 = RN(x*y)
+// with y = RN(1/denom), then two FMA corrections q <- RN(q + RN(x - q*denom)*y)
+// (the residual x - q*denom is exact in an FMA). After the first correction
+// q is a faithful quotient (relative error ~2^-105 before rounding), and y has
+// relative error below 2^-53, so by Markstein's theorem the second correction
+// returns RN(x/denom). denom > 0, so the quotient has x's sign (the copysign
+// keeps -0/denom = -0, which the corrections would turn into +0). Finite,
+// normal operands (pressure sums): no over/underflow. Checked against the
+// hardware divide in tests/test_division.py (random and adversarial denominators).
+__device__ __forceinline__ double div_denom(const Coef& c, double x) {
+  const double d = c.denom, y = c.rdenom;
+  double q = x * y;
+  q = fma(fma(-q, d, x), y, q);
+  q = fma(fma(-q, d, x), y, q);
+  return copysign(q, x);
+}
+
 template <int CASE>
 __device__ __forceinline__ double sor_update(const Coef& c, int nx, int ny, int j, int i, double pc, double pW,
                                              double pE, double pS, double pN, double fc) {
@@ -421,7 +439,7 @@ __device__ __forceinline__ double sor_update(const Coef& c, int nx, int ny, int 
     return pc * c.one_m_omega + om * ((tE + tW) + (tN + pS) - fc * c.h2);
   } else {
     const double sum = c.idx2 * (pE + pW) + c.idy2 * (pN + pS);
-    const double gs = (sum - fc) / c.denom;
+    const double gs = div_denom(c, sum - fc);  // (sum - fc) / denom
     return c.one_m_omega * pc + c.omega * gs;
   }
 }
@@ -529,10 +547,14 @@ struct WaveCtx {
   bool pair_ok, out_lane, icol_a, icol_b, open_a, open_b;
   __device__ bool fl_a(int j) const { return icol_a && j >= 1 && j <= g.ny && (open_a || j <= c.inlet_jmax); }
   __device__ bool fl_b(int j) const { return icol_b && j >= 1 && j <= g.ny && (open_b || j <= c.inlet_jmax); }
+  // boundary-column waves: row and column clamped to stored memory, no select
+  // on the value (a select waits for the load and defeats the prefetch): the
+  // values of rows / lanes outside the stored grid feed only cells that are
+  // never updated, refreshed or stored (ghost rows' refresh reads their inner
+  // neighbour; halo lanes' cells are masked)
   __device__ double2 ld(const double* base, int R) const {
     const int Rc = min(max(R, rmin), rmax);
-    const double2 v = *reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * (size_t)g.pitch + gic);
-    return (pair_ok && R >= rmin && R <= rmax) ? v : make_double2(0.0, 0.0);
+    return *reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * (size_t)g.pitch + gic);
   }
   // interior waves: every column stored, rows clamped (wave-uniform scalar math)
   __device__ double2 ld_fast(const double* base, int R) const {
@@ -795,7 +817,7 @@ __device__ __forceinline__ double sor_interior(const Coef& c, double pc, double 
                                                double fc) {
   if (CASE == CAVITY) return pc * c.one_m_omega + c.om_nc[4] * ((pE + pW) + (pN + pS) - fc * c.h2);
   const double sum = c.idx2 * (pE + pW) + c.idy2 * (pN + pS);
-  const double gs = (sum - fc) / c.denom;
+  const double gs = div_denom(c, sum - fc);  // (sum - fc) / denom
   return c.one_m_omega * pc + c.omega * gs;
 }
 template <int CASE>
@@ -1328,7 +1350,16 @@ __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAI
   // interior-column wave: all 128 columns are fluid cells with fluid
   // neighbours (rows are handled row-uniformly inside the fast march)
   const int c0 = ctile * PAIR_TWC - H;
-  const bool cols_in = c0 >= 1 && c0 + 127 <= g.nx && (CASE != BACKSTEP || c0 > c.step_i + 1);
+  bool cols_in = c0 >= 1 && c0 + 127 <= g.nx && (CASE != BACKSTEP || c0 > c.step_i + 1);
+  if (CASE == BACKSTEP && c0 >= 1 && c0 + 127 <= g.nx && !cols_in) {
+    // column tiles over the solid block (i <= step_i, j > inlet_jmax): a band
+    // whose march (rows y0-10 .. y1+10 cover the pipeline and its neighbours)
+    // stays below the block is plain fluid (interior path); one that stays
+    // inside the block, away from fluid and from ghost rows, is never updated
+    // or refreshed (both buffers hold its values): nothing to do
+    if (y1 + 10 <= c.inlet_jmax - 1) cols_in = true;
+    else if (y0 - 10 >= c.inlet_jmax + 2 && y1 + 10 <= g.ny && c0 + 128 <= c.step_i - 1) return;
+  }
   const bool up = (flags & 1) && (band & 1);
   // flags bit 4 / bit 5 (timing diagnostics only): never / always take the interior path
   const bool fast = (flags & 32) || (!(flags & 16) && cols_in);

@@ -69,6 +69,7 @@ static Coef make_coef(const cfd_params& p) {
   for (int n = 0; n < 5; ++n) c.om_nc[n] = (n > 0) ? p.omega / n : 0.0;
   c.h2 = p.dx * p.dx;
   c.denom = 2.0 * (c.idx2 + c.idy2);
+  c.rdenom = 1.0 / c.denom;
   c.cav_src = (1.0 / p.dt) * p.rho;
   c.open_src = p.rho / p.dt;
   c.cav_corr = (p.dt / p.dx) * p.rho;
@@ -211,6 +212,7 @@ class Solver {
         if (const char* e = std::getenv("CFD_LEXW_WAVES")) resident_lexw_waves = std::max(64, std::atoi(e));
       }
       if (const char* e = std::getenv("CFD_PAIR_EDGE_PCT")) pair_edge_pct = std::max(10, std::min(100, std::atoi(e)));
+      if (const char* e = std::getenv("CFD_MARCH_MIN_TH")) march_min_th = std::max(1, std::atoi(e));  // tuning
       resident_pair_waves = pps * 4 * prop.multiProcessorCount;
     }
     pitch = ((P.nx + 3) + 15) / 16 * 16;  // >= nx+3: column pairs (gi, gi+1) stay inside a row
