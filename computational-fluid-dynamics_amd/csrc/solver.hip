@@ -18,6 +18,7 @@
 #include "internal.hpp"
 #include "kernels.hpp"
 #include "lexw.hpp"
+#include "small.hpp"
 
 namespace cfd {
 
@@ -973,6 +974,54 @@ class Solver {
     }
   }
 
+  // red-black solve of a reference-sized grid in one persistent workgroup
+  // (small.hpp): one strip, no ranks, p fits the LDS (CFD_SMALL=0: never)
+  bool use_small() const {
+    const char* e = std::getenv("CFD_SMALL");
+    const bool off = e && std::atoi(e) == 0;
+    return !off && P.ordering == CFD_ORDER_RB && S.size() == 1 && !comm &&
+           (long long)(P.nx + 2) * (P.ny + 2) <= SMALL_CELLS;
+  }
+
+  void solve_small(cfd_step_info* out) {
+    Strip& s = S[0];
+    double* X = s.b[pbuf(pcur)];
+    if (P.case_id == CFD_CAVITY)  // cavity-01.cpp:610-611: each solve starts from a zero field
+      HIPC(hipMemsetAsync(X, 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
+    solve_tolerance();
+    int* d_it = stop;
+    double* d_res = total + 2;
+    HIPC(hipEventRecord(ev_a, st));
+    const int ce = std::max(1, P.check_every);
+    const bool fl = 2LL * (P.nx + 2) * (P.ny + 2) <= SMALL_CELLS;  // f in LDS too
+#define CFD_SMALL_LAUNCH(CASE)                                                                                  \
+  if (fl) poisson_small_kernel<CASE, true><<<1, SMALL_THREADS, 0, st>>>(s.g, C, X, s.b[B_F], tolv, P.max_iters, ce, \
+                                                                        d_it, d_res);                          \
+  else poisson_small_kernel<CASE, false><<<1, SMALL_THREADS, 0, st>>>(s.g, C, X, s.b[B_F], tolv, P.max_iters, ce,  \
+                                                                       d_it, d_res)
+    if (P.case_id == CFD_CAVITY) { CFD_SMALL_LAUNCH(CAVITY); }
+    else if (P.case_id == CFD_CHANNEL) { CFD_SMALL_LAUNCH(CHANNEL); }
+    else { CFD_SMALL_LAUNCH(BACKSTEP); }
+#undef CFD_SMALL_LAUNCH
+    check_launch("poisson_small");
+    HIPC(hipEventRecord(ev_b, st));
+    int iters = 0;
+    double res = 0;
+    HIPC(hipMemcpyAsync(&iters, d_it, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(&res, d_res, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
+    T.poisson_ms += ms;
+    T.poisson_launches += 1;
+    T.poisson_sweeps += iters;
+    T.poisson_cell_updates += (long long)P.nx * P.ny * iters;
+    if (out) {
+      out->sor_iterations = iters;
+      out->residual = res;
+    }
+  }
+
   void solve(cfd_step_info* out) {
     if (use_lexw()) {
       solve_lexw(out);
@@ -980,6 +1029,10 @@ class Solver {
     }
     if (P.ordering == CFD_ORDER_LEX) {
       solve_lex(out);
+      return;
+    }
+    if (use_small()) {
+      solve_small(out);
       return;
     }
     const int base = pcur;
