@@ -123,6 +123,22 @@ __device__ __forceinline__ double block_sum(double v) {
   return s;  // valid in thread 0
 }
 
+// Row neighbours across lanes (wave shifts).
+// bound_ctrl: the lane without a source (0 resp. 63) reads 0, with no
+// zero-initialised destination to merge into (one v_mov_dpp per dword)
+__device__ __forceinline__ double dpp_from_left(double v) {  // lane l receives lane l-1 (wave_shr:1)
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_mov_dpp(lo, 0x138, 0xf, 0xf, true);
+  hi = __builtin_amdgcn_mov_dpp(hi, 0x138, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_from_right(double v) {  // lane l receives lane l+1 (wave_shl:1)
+  int lo = __double2loint(v), hi = __double2hiint(v);
+  lo = __builtin_amdgcn_mov_dpp(lo, 0x130, 0xf, 0xf, true);
+  hi = __builtin_amdgcn_mov_dpp(hi, 0x130, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+
 // ------------------------------------------------------------------ BCs --
 
 // cavity-01.cpp:523-543: moving lid + no-slip walls by ghost reflection.
@@ -212,49 +228,110 @@ __global__ void bc_step_faces_kernel(Geo g, Coef c, double* __restrict__ u, doub
 // ------------------------------------------------------------ predictor --
 
 // cavity-01.cpp:548-603 / channel-01.cpp:546-603 / backwards_step-01.cpp:745-820.
+// Row march (like the SOR kernels): a wave owns 128 columns (2 per lane,
+// 16-byte loads) and walks down a band of `th` rows keeping rows j-1, j, j+1
+// of u and v in registers; column neighbours move between lanes by DPP. Each
+// row costs one load of u and of v and the stores of u*, v* (32 B per cell plus
+// 2 halo rows per band and 2 halo columns per 128). Output columns: the
+// wave's columns 1..126 (TENT_TWC per tile). Same expressions in the same
+// order as the reference loops, hence the same bits.
+constexpr int TENT_TWC = 126;
 __global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const double* __restrict__ u,
                                                         const double* __restrict__ v, double* __restrict__ us,
-                                                        double* __restrict__ vs) {
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+                                                        double* __restrict__ vs, int th, int ctiles) {
+  const int lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int ctile = tile % ctiles, band = tile / ctiles;
+  const int y0 = g.j0 + band * th, y1 = min(y0 + th, g.j1 + 1);
+  if (y0 >= y1) return;
   const int nx = g.nx, ny = g.ny;
-  if (j > g.j1 || j < 1 || j > ny) return;
   const bool step = c.case_id == BACKSTEP;
-  const size_t o = at(g, j, i);
+  const int gi = ctile * TENT_TWC + 2 * lane;      // this lane's columns gi (a), gi + 1 (b)
+  const int gic = min(gi, g.pitch - 2);             // (lanes past the row read a valid pair)
   const size_t P = (size_t)g.pitch;
-  if (i >= 1 && i <= nx - 1) {
-    const double cc = u[o];
-    const double uE = u[o + 1], uW = u[o - 1];
-    const double uN = u[o + P], uS = u[o - P];
-    const double diff = c.nu * ((uE - 2.0 * cc + uW) * c.idx2 + (uN - 2.0 * cc + uS) * c.idy2);
-    const double ue = 0.5 * (cc + uE);
-    const double uw = 0.5 * (uW + cc);
-    const double cx = (ue * ue - uw * uw) * c.idx;
-    const double vn = 0.5 * (v[o] + v[o + 1]);
-    const double vso = 0.5 * (v[o - P] + v[o - P + 1]);
-    const double un = 0.5 * (uN + cc);
-    const double uso = 0.5 * (uS + cc);
-    const double cy = (vn * un - vso * uso) * c.idy;
-    const double val = cc + c.dt * (diff - cx - cy);
-    const bool valid = !step || is_fluid(c, nx, ny, j, i) || is_fluid(c, nx, ny, j, i + 1);
-    us[o] = valid ? val : 0.0;
-  }
-  if (i >= 1 && i <= nx && j <= ny - 1) {
-    const double cc = v[o];
-    const double vE = v[o + 1], vW = v[o - 1];
-    const double vN = v[o + P], vS = v[o - P];
-    const double diff = c.nu * ((vE - 2.0 * cc + vW) * c.idx2 + (vN - 2.0 * cc + vS) * c.idy2);
-    const double vn = 0.5 * (cc + vN);
-    const double vso = 0.5 * (vS + cc);
-    const double cy = (vn * vn - vso * vso) * c.idy;
-    const double ue = 0.5 * (u[o] + u[o + P]);
-    const double uw = 0.5 * (u[o - 1] + u[o + P - 1]);
-    const double ve = 0.5 * (cc + vE);
-    const double vw = 0.5 * (vW + cc);
-    const double cx = (ue * ve - uw * vw) * c.idx;
-    const double val = cc + c.dt * (diff - cy - cx);
-    const bool valid = !step || is_fluid(c, nx, ny, j, i) || is_fluid(c, nx, ny, j + 1, i);
-    vs[o] = valid ? val : 0.0;
+  auto ld = [&](const double* base, int j) {
+    return *reinterpret_cast<const double2*>(base + (size_t)(j - g.row_lo) * P + gic);
+  };
+  // output cells: a of lanes 1..63, b of lanes 0..62 (their row neighbours are in the wave)
+  const bool out_a = lane >= 1 && gi <= nx, out_b = lane <= 62 && gi + 1 <= nx;
+  // rows j+1 .. j+3 of u and v in flight (clamped to the strip's stored rows:
+  // rows past y1 are never consumed)
+  const int rlast = g.row_lo + g.nrows - 1;
+  auto ldc = [&](const double* base, int j) { return ld(base, min(j, rlast)); };
+  double2 um = ld(u, y0 - 1), uc = ld(u, y0), vm = ld(v, y0 - 1), vc = ld(v, y0);
+  double2 uq0 = ldc(u, y0 + 1), vq0 = ldc(v, y0 + 1), uq1 = ldc(u, y0 + 2), vq1 = ldc(v, y0 + 2);
+  double2 uq2 = ldc(u, y0 + 3), vq2 = ldc(v, y0 + 3);
+  for (int j = y0; j < y1; ++j) {
+    const double2 up = uq0, vp = vq0;
+    uq0 = uq1; vq0 = vq1; uq1 = uq2; vq1 = vq2;
+    uq2 = ldc(u, j + 4);
+    vq2 = ldc(v, j + 4);
+    const double uWa = dpp_from_left(uc.y), uEb = dpp_from_right(uc.x);
+    const double vEb = dpp_from_right(vc.x), vmEb = dpp_from_right(vm.x);
+    const double vWa = dpp_from_left(vc.y), upWa = dpp_from_left(up.y);
+    double* usr = us + (size_t)(j - g.row_lo) * P;
+    double* vsr = vs + (size_t)(j - g.row_lo) * P;
+    double usv[2], vsv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = gi + h;
+      // u* on the face (j, i): cells 1..nx-1
+      {
+        const double cc = h == 0 ? uc.x : uc.y;
+        const double uE = h == 0 ? uc.y : uEb, uW = h == 0 ? uWa : uc.x;
+        const double uN = h == 0 ? up.x : up.y, uS = h == 0 ? um.x : um.y;
+        const double diff = c.nu * ((uE - 2.0 * cc + uW) * c.idx2 + (uN - 2.0 * cc + uS) * c.idy2);
+        const double ue = 0.5 * (cc + uE);
+        const double uw = 0.5 * (uW + cc);
+        const double cx = (ue * ue - uw * uw) * c.idx;
+        const double vn = 0.5 * ((h == 0 ? vc.x : vc.y) + (h == 0 ? vc.y : vEb));
+        const double vso = 0.5 * ((h == 0 ? vm.x : vm.y) + (h == 0 ? vm.y : vmEb));
+        const double un = 0.5 * (uN + cc);
+        const double uso = 0.5 * (uS + cc);
+        const double cy = (vn * un - vso * uso) * c.idy;
+        const double val = cc + c.dt * (diff - cx - cy);
+        const bool valid = !step || is_fluid(c, nx, ny, j, i) || is_fluid(c, nx, ny, j, i + 1);
+        usv[h] = valid ? val : 0.0;
+      }
+      // v* on the face (j, i): rows 1..ny-1
+      {
+        const double cc = h == 0 ? vc.x : vc.y;
+        const double vE = h == 0 ? vc.y : vEb, vW = h == 0 ? vWa : vc.x;
+        const double vN = h == 0 ? vp.x : vp.y, vS = h == 0 ? vm.x : vm.y;
+        const double diff = c.nu * ((vE - 2.0 * cc + vW) * c.idx2 + (vN - 2.0 * cc + vS) * c.idy2);
+        const double vn = 0.5 * (cc + vN);
+        const double vso = 0.5 * (vS + cc);
+        const double cy = (vn * vn - vso * vso) * c.idy;
+        const double ue = 0.5 * ((h == 0 ? uc.x : uc.y) + (h == 0 ? up.x : up.y));
+        const double uw = 0.5 * ((h == 0 ? uWa : uc.x) + (h == 0 ? upWa : up.x));
+        const double ve = 0.5 * (cc + vE);
+        const double vw = 0.5 * (vW + cc);
+        const double cx = (ue * ve - uw * vw) * c.idx;
+        const double val = cc + c.dt * (diff - cy - cx);
+        const bool valid = !step || is_fluid(c, nx, ny, j, i) || is_fluid(c, nx, ny, j + 1, i);
+        vsv[h] = valid ? val : 0.0;
+      }
+    }
+    // 16-byte stores where both cells of the lane are written (coalesced rows),
+    // single cells at the tile and grid edges
+    const bool ua = out_a && gi >= 1 && gi <= nx - 1, ub = out_b && gi + 1 >= 1 && gi + 1 <= nx - 1;
+    const bool va = out_a && gi >= 1 && j <= ny - 1, vb = out_b && gi + 1 <= nx && j <= ny - 1;
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    if (ua && ub) {
+      d2v w = {usv[0], usv[1]};
+      *reinterpret_cast<d2v*>(usr + gi) = w;
+    } else {
+      if (ua) usr[gi] = usv[0];
+      if (ub) usr[gi + 1] = usv[1];
+    }
+    if (va && vb) {
+      d2v w = {vsv[0], vsv[1]};
+      *reinterpret_cast<d2v*>(vsr + gi) = w;
+    } else {
+      if (va) vsr[gi] = vsv[0];
+      if (vb) vsr[gi + 1] = vsv[1];
+    }
+    um = uc; uc = up; vm = vc; vc = vp;
   }
 }
 
@@ -309,9 +386,12 @@ __global__ __launch_bounds__(256) void thermal_kernel(Geo g, Coef c, const doubl
 // (f and, for the open cases, its per-block partial sum for the mean).
 // Straight-line form: the address is formed once and the value selected, so
 // no lane's store depends on which branch the wave took.
+// The cavity's tolerance input max|f| (cavity-01.cpp:628) is reduced in the
+// same pass into the srcmax shards (the open cases reduce it after the mean
+// removal, subtract_mean_kernel): one read of f fewer per timestep.
 __global__ __launch_bounds__(256) void source_kernel(Geo g, Coef c, const double* __restrict__ us,
                                                      const double* __restrict__ vs, double* __restrict__ f,
-                                                     double* __restrict__ partials) {
+                                                     double* __restrict__ partials, double* __restrict__ srcmax) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
   const int nx = g.nx, ny = g.ny;
@@ -330,6 +410,8 @@ __global__ __launch_bounds__(256) void source_kernel(Geo g, Coef c, const double
   if (c.case_id != CAVITY) {
     const double s = block_sum<256>(val);
     if (threadIdx.x == 0) partials[blockIdx.y * gridDim.x + blockIdx.x] = s;
+  } else {
+    block_max_to_shard<256>(fabs(val), srcmax, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
   }
 }
 
@@ -343,20 +425,27 @@ __global__ __launch_bounds__(256) void sum_partials_kernel(const double* __restr
 }
 
 // channel-01.cpp:621-628 / backwards_step-01.cpp:844-865: subtract the mean
-// over fluid cells.
+// over fluid cells, and reduce max|f| (channel-01.cpp:643-646,
+// backwards_step-01.cpp:880-887) into the srcmax shards in the same pass.
 __global__ __launch_bounds__(256) void subtract_mean_kernel(Geo g, Coef c, double* __restrict__ f,
-                                                            const double* __restrict__ total, double count) {
+                                                            const double* __restrict__ total, double count,
+                                                            double* __restrict__ srcmax) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
   const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
   const int nx = g.nx, ny = g.ny;
+  double m = 0.0;
   if (i >= 1 && i <= nx && j >= 1 && j <= ny && j <= g.j1 && is_fluid(c, nx, ny, j, i)) {
     const double mean = total[0] / count;
-    f[at(g, j, i)] = f[at(g, j, i)] - mean;
+    const double v = f[at(g, j, i)] - mean;
+    f[at(g, j, i)] = v;
+    m = fabs(v);
   }
+  block_max_to_shard<256>(m, srcmax, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
 }
 
 // max|f| over the fluid cells the solve iterates on: cavity-01.cpp:628,
-// channel-01.cpp:643-646, backwards_step-01.cpp:880-887.
+// channel-01.cpp:643-646, backwards_step-01.cpp:880-887 (when the source was
+// set from the host rather than built by source_kernel / subtract_mean_kernel).
 __global__ __launch_bounds__(256) void srcmax_kernel(Geo g, Coef c, const double* __restrict__ f,
                                                      double* __restrict__ srcmax) {
   const int i = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -489,21 +578,6 @@ __device__ __forceinline__ bool refresh_value(const Coef& c, int nx, int ny, int
 // writes 120 columns. At front row R one step loads p_in(R), f(R-1); updates
 // red at R-1, black at R-2; refreshes ghosts / solids at R-3; computes the
 // residual and stores at R-4. Rows R+1..R+4 of p_in and f are in flight.
-
-// bound_ctrl: the lane without a source (0 resp. 63) reads 0, with no
-// zero-initialised destination to merge into (one v_mov_dpp per dword)
-__device__ __forceinline__ double dpp_from_left(double v) {  // lane l receives lane l-1 (wave_shr:1)
-  int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_mov_dpp(lo, 0x138, 0xf, 0xf, true);
-  hi = __builtin_amdgcn_mov_dpp(hi, 0x138, 0xf, 0xf, true);
-  return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double dpp_from_right(double v) {  // lane l receives lane l+1 (wave_shl:1)
-  int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_mov_dpp(lo, 0x130, 0xf, 0xf, true);
-  hi = __builtin_amdgcn_mov_dpp(hi, 0x130, 0xf, 0xf, true);
-  return __hiloint2double(hi, lo);
-}
 
 // Residual magnitude for the march kernels: as residual_at, but the cavity's
 // 0/1 indicator products are selects. Only |r| is used (max-norm), and

@@ -458,15 +458,22 @@ class Solver {
       exchange(B_V, 1);
     }
     for (auto& s : S) {
-      tentative_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_U], s.b[B_V], s.b[B_US], s.b[B_VS]);
+      const int ct = (P.nx + TENT_TWC - 1) / TENT_TWC, rows = s.g.j1 - s.g.j0 + 1;
+      static const int tth = std::getenv("CFD_TENT_TH") ? std::max(4, std::atoi(std::getenv("CFD_TENT_TH"))) : 64;
+      const int th = std::max(1, std::min(tth, rows));  // rows per band (tuned: 64)
+      const int tiles = ct * ((rows + th - 1) / th);
+      tentative_kernel<<<(tiles + 3) / 4, 256, 0, st>>>(s.g, C, s.b[B_U], s.b[B_V], s.b[B_US], s.b[B_VS], th, ct);
       check_launch("tentative");
     }
   }
 
+  bool srcmax_ready = false;  // srcmax holds max|f| of the current source (reduced by the source passes)
+
   void build_source() {
+    HIPC(hipMemsetAsync(srcmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
     if (multi()) exchange(B_VS, 1);
     for (auto& s : S) {
-      source_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_US], s.b[B_VS], s.b[B_F], partials + s.part_off);
+      source_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_US], s.b[B_VS], s.b[B_F], partials + s.part_off, srcmax);
       check_launch("source");
     }
     if (P.case_id != CFD_CAVITY) {
@@ -478,18 +485,22 @@ class Solver {
       check_launch("sum_partials");
       if (comm && comm->nranks > 1) comm_allreduce_sum(comm, total, 1, st);
       for (auto& s : S) {
-        subtract_mean_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_F], total, fluid_count);
+        subtract_mean_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_F], total, fluid_count, srcmax);
         check_launch("subtract_mean");
       }
     }
+    srcmax_ready = true;
   }
 
   // Tolerance from the current source (computed inside the reference's solve).
   void solve_tolerance() {
-    HIPC(hipMemsetAsync(srcmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
-    for (auto& s : S) {
-      srcmax_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_F], srcmax);
-      check_launch("srcmax");
+    if (!srcmax_ready) {  // the source came from the host: reduce it here
+      HIPC(hipMemsetAsync(srcmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
+      for (auto& s : S) {
+        srcmax_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_F], srcmax);
+        check_launch("srcmax");
+      }
+      srcmax_ready = true;
     }
     if (comm && comm->nranks > 1) comm_allreduce_max(comm, srcmax, RES_SHARDS * SHARD_STRIDE, st);
     tol_kernel<<<1, 64, 0, st>>>(C, srcmax, tolv);
@@ -1281,6 +1292,7 @@ class Solver {
     owned_field_rows(field, first, last);
     if (count != (size_t)(last - first + 1) * cols) throw Error(CFD_E_ARG, "host buffer size does not match field shape");
     const int b = field_buf(field);
+    if (chost && b == B_F) srcmax_ready = false;  // a new source from the host
     for (auto& s : S) {
       const int r0 = s.g.wj0, r1 = std::min(s.g.wj1, rows - 1);
       if (r1 < r0) continue;

@@ -77,8 +77,9 @@ def test_lex_vtk_frame_byte_identical(tmp_path):
     assert hashlib.sha256(fn.read_bytes()).hexdigest() == LOGS["cavity"]["vtk_sha256"]["100"]
 
 
-def test_lex_rejects_strips():
+def test_open_case_lex_rejects_strips():
+    """The open cases' reference order runs in one workgroup (poisson_lex_kernel):
+    one strip only. (The cavity's runs on strips: tests/test_gpu_lexw.py.)"""
     with pytest.raises(C._lib.CfdError if hasattr(C, "_lib") else Exception):
-        g = C.CavitySolver(C.reference_defaults("cavity"), ordering="lex", n_strips=2)
-        g.applyBoundaryConditions()
+        g = C.ChannelSolver(C.reference_defaults("channel"), ordering="lex", n_strips=2)
         g.step()

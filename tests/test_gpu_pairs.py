@@ -20,6 +20,15 @@ import cfd_amd as C  # noqa: E402
 import oracle as O  # noqa: E402
 from test_gpu_parity import assert_bits  # noqa: E402
 
+
+
+@pytest.fixture(autouse=True)
+def multi_launch_path(monkeypatch):
+    """These are tests of the multi-launch plan: reference-sized grids would
+    otherwise take the one-workgroup solve (small.hpp, tests/test_gpu_small.py)."""
+    monkeypatch.setenv("CFD_SMALL", "0")
+
+
 SOLVERS = {"cavity": C.CavitySolver, "channel": C.ChannelSolver, "backwards_step": C.BackwardsStepSolver}
 FIELDS = ("p", "u", "v")
 
