@@ -9,28 +9,36 @@
 // H-1; E, N reached k-1 at H-1 and move on only at H+1). So the lexicographic
 // solve of K iterations is 2K + nx + ny - 2 red-black half-sweeps in which cell
 // (j,i) is updated only while i+j <= H <= i+j+2(K-1): a ramp at the start and
-// the end, plain red-black in between (scripts/ in DESIGN.md §2 checks the
-// identity against the oracle).
+// the end, plain red-black in between (tests/test_gpu_lexw.py checks the
+// result bit for bit against the oracle's restatement of the reference loop).
 //
-// The kernel is the cavity's temporal-blocked march (kernels.hpp, cav_march):
-// one wave = 128 columns marching up a band of rows, NS sweeps (2NS half-
-// sweeps) per launch, red at R-(2S+1), black at R-(2S+2). What differs:
-//  * activity masks on tiles that straddle the ramps (FULL tiles need none,
-//    tiles with nothing to do are skipped);
-//  * the residual of iteration k (cavity-01.cpp:659-677) needs each cell's
-//    neighbours at iteration k, i.e. a red cell's black neighbours W, S before
-//    and E, N after the black half-sweep that follows it; a black cell's red
-//    neighbours before / after the next red half-sweep. The march keeps each
-//    sweep's input rows (ring `in`) next to its output rows (ring `w`) and
-//    evaluates, at row R-(2S+3): red cells of sweep S and black cells of sweep
-//    S-1 (black cells of a launch's last sweep: in the next launch's sweep 0).
-//  * iteration numbers vary along the grid (k = (H - i - j)/2 + 1), so a
-//    residual is not a per-launch max: each cell contributes to slot k. The
-//    loop's test `res > tol` only needs, per k, whether some cell exceeds the
-//    tolerance: a wave ballot per row and sweep goes into a per-wave bit window
-//    (slots move by one lane every two rows), flushed once per wave into a
-//    global per-slot bitset (atomicOr). The reported residual (max-norm of the
-//    last iteration) is recomputed from the final field by a separate pass.
+// The kernel is a temporal-blocked wave march like the cavity's red-black one
+// (kernels.hpp cav_march): one wave = 128 columns (2 per lane, DPP row
+// neighbours) marching DOWN a band of rows, NS sweeps (2NS half-sweeps) per
+// launch, each sweep's red and black rows a fixed distance behind the front
+// row. What differs:
+//  * activity: a launch whose every cell is active in every half-sweep it
+//    evaluates (the steady phase) runs the plain march; the launches of the
+//    two ramps (the first and last (nx+ny)/2NS of a solve) tile only the rows
+//    they touch (LexRamp) and mask per cell only in tiles that straddle a ramp
+//    front (LX_ACT: three compares per march step, shared by all rows);
+//  * residuals: iteration k's residual (cavity-01.cpp:659-677) needs each
+//    cell's W, S neighbours before and E, N after the half-sweep that follows
+//    it. Marching down, those are exactly the old and new values of the row
+//    being updated, so each row update also evaluates the other colour's
+//    residual in the same registers (lx_row). A lane's contributions at front
+//    row R all belong to iteration Bd(R) - lane;
+//  * convergence: the loop's test `res > tol` only needs, per iteration,
+//    whether some cell exceeds the tolerance. Each lane keeps one bit per
+//    march step (a pinned per-row flag, no max in the loop), the lanes' masks
+//    are merged along the diagonals once per wave and OR-ed into a global
+//    per-iteration bitset (8 shards), which the next launches test in order.
+//    The reported residual (max-norm of the last iteration) is recomputed from
+//    the final field (cavity_resmax_kernel); a stop at k < K replays the solve
+//    from its initial field with K = k;
+//  * straight-line rows: row-uniform conditions (updated row, top row, output
+//    row) become scalar coefficients / thresholds, never branches: branches on
+//    them split the march loop and serialised its loads (2x slower).
 #pragma once
 
 #include "kernels.hpp"

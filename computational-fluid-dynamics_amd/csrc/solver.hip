@@ -763,8 +763,7 @@ class Solver {
     const int ne = pl.ctiles >= 2 ? 2 : 1;
     int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
     LexRamp rp{};
-    static const bool ramp_all = std::getenv("CFD_LEXW_RAMP_TILING") != nullptr;  // diagnostic
-    if (!steady || ramp_all) {
+    if (!steady) {
       // ramp launch: tile only the rows it touches (lexw_rows), bands of the
       // shortest height whose tiles fit one resident round, at most the
       // steady plan's (at that every ramp launch fits: it touches fewer rows)
@@ -808,12 +807,11 @@ class Solver {
       while (th < pl.th && ntiles > waves) ntiles = build(th += 10);
       if (th > pl.th) ntiles = build(th = std::max(pl.th, (rh - rl) / LEXW_RAMP_BANDS + 1));
       if (pl.ctiles > 255 || ntiles >= 65536) throw Error(CFD_E_ARG, "lexicographic ordering: grid too wide");
-    }    if (ntiles == 0) return;
+    }
+    if (ntiles == 0) return;
     const dim3 grid((ntiles + 3) / 4);
 #define CFD_LEXW_LAUNCH(NS, R) \
   poisson_lexw_kernel<NS, R><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl, rp)
-    static const bool all_ramp_kernel = std::getenv("CFD_LEXW_RAMP_KERNEL") != nullptr;  // diagnostic
-    if (all_ramp_kernel) steady = false;
     if (ns == 1) { if (steady) CFD_LEXW_LAUNCH(1, false); else CFD_LEXW_LAUNCH(1, true); }
     else if (ns == 2) { if (steady) CFD_LEXW_LAUNCH(2, false); else CFD_LEXW_LAUNCH(2, true); }
     else { if (steady) CFD_LEXW_LAUNCH(3, false); else CFD_LEXW_LAUNCH(3, true); }
