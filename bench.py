@@ -112,7 +112,21 @@ def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch
             "steady_launches_per_step": round(tm.poisson_steady_launches / args.lex_steps, 1),
             "steady_launch_us": round(steady_ms * 1e3, 2) if tm.poisson_steady_launches else None,
             "steady_achieved_GBs": round(achieved, 1) if achieved else None,
-            "steady_frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None}
+            "steady_frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "steady_traffic": pmc_traffic("r2_lexw_pmc.json", cp.nx, cells_per_launch // (cp.nx + 2), 3)}
+
+
+def pmc_traffic(name: str, nx: int, rows: int, sweeps: int):
+    """HBM bytes per SOR launch from a committed PMC pass (profiles/, made by
+    scripts/pmc_traffic.sh + pmc_traffic.py on the same workload), or None."""
+    path = os.path.join(ROOT, "profiles", name)
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if d.get("nx") == nx and d.get("rows") == rows and d.get("sweeps_per_launch", 1) == sweeps:
+        return d.get("hbm_bytes_per_launch")
+    return None
 
 
 def kcase_of(case: str) -> str:
@@ -233,16 +247,9 @@ def main() -> int:
         # the same launch measured as if each sweep streamed its own 24 B/cell
         # (the unfused algorithm's traffic): the temporal-blocking gain
         effective = achieved * sweeps_per_launch
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "poisson_pmc.json")
-        if os.path.exists(pmc):
-            try:
-                d = json.load(open(pmc))
-                if (d.get("nx") == cp.nx and d.get("rows") == wrows
-                        and d.get("sweeps_per_launch", 1) == round(sweeps_per_launch)):
-                    traffic = d.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        traffic = None if lexw else pmc_traffic("poisson_pmc.json", cp.nx, wrows, round(sweeps_per_launch))
+        if lexw:
+            traffic = pmc_traffic("r2_lexw_pmc.json", cp.nx, wrows, round(sweeps_per_launch))
         mlups = updates / elapsed / 1e6
         kcase = kcase_of(args.case)
         rows_here = g1 - g0 + 1
