@@ -252,6 +252,13 @@ def main() -> int:
             traffic = pmc_traffic("r2_lexw_pmc.json", cp.nx, wrows, round(sweeps_per_launch))
         mlups = updates / elapsed / 1e6
         kcase = kcase_of(args.case)
+        # red-black cavity 3-sweep launches: proof-mode convergence test
+        # (CFD_PROOF=0 evaluates the residual in every sweep)
+        proof = (not lexw and kcase == "cavity" and round(sweeps_per_launch) >= 3
+                 and os.environ.get("CFD_PROOF", "1") != "0")
+        if proof:
+            traffic = pmc_traffic(f"r2_proof{round(sweeps_per_launch)}_pmc.json", cp.nx, wrows,
+                                  round(sweeps_per_launch))
         rows_here = g1 - g0 + 1
         per_gpu = (f"{cp.nx}x{rows_here} fp64 cells per GPU (global {cp.nx}x{cp.ny} split over {n_gpus} GPUs)"
                    if strong else f"{cp.nx}x{args.ny} fp64 cells per GPU (global {cp.nx}x{cp.ny})")
@@ -275,6 +282,7 @@ def main() -> int:
                             f"cap {cp.max_iters} sweeps/step, {'strong' if strong else 'weak'} scaling",
                 "nx": cp.nx, "ny_per_gpu": rows_here, "global_ny": cp.ny,
                 "parallelism": f"strip{n_gpus}", "check_every": check_every, "ordering": args.ordering,
+                "convergence_test": "proof" if proof else "residual",
             },
             "rccl_ranks": comm_info["nranks"] if comm_info else None,
             "transport": (comm_info["transport"] if comm_info else "none (1 GPU)"),
@@ -282,6 +290,7 @@ def main() -> int:
             "sor_iterations_per_step": iters,
             "sor_cap_hits": sum(1 for i in iters if i >= cp.max_iters),
             "final_residual_per_step": [float(f"{r:.6e}") for r in resids],
+            "proof_fallbacks": int(tm.proof_fallbacks),
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -290,6 +299,7 @@ def main() -> int:
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel": (f"poisson_lexw_kernel<{round(sweeps_per_launch)}>" if lexw
+                           else f"poisson_multi_kernel<{kcase},{round(sweeps_per_launch)},proof>" if proof
                            else f"poisson_multi_kernel<{kcase},3>" if sweeps_per_launch > 2.5
                            else f"poisson_multi_kernel<{kcase},2>" if sweeps_per_launch > 1.5
                            else f"poisson_wave_kernel<{kcase}>"),

@@ -59,7 +59,8 @@ class Timing(ctypes.Structure):
                 ("poisson_cell_updates", ctypes.c_longlong), ("step_ms", ctypes.c_double),
                 ("steps", ctypes.c_longlong), ("poisson_sweeps", ctypes.c_longlong),
                 ("poisson_overlapped", ctypes.c_longlong), ("poisson_steady_ms", ctypes.c_double),
-                ("poisson_steady_launches", ctypes.c_longlong)]
+                ("poisson_steady_launches", ctypes.c_longlong),
+                ("proof_fallbacks", ctypes.c_longlong)]
 
 
 # every symbol include/cfd_amd.h declares: name -> (restype, argtypes)

@@ -53,6 +53,7 @@ struct Coef {
   double cav_corr;         // cavity: (dt/h) * rho           (cavity-01.cpp:696,701)
   double open_cu, open_cv; // open:   dt/(rho*dx), dt/(rho*dy) (channel-01.cpp:697,701)
   double tol_factor, abs_tol;
+  double proof_k;          // cavity proof-mode test: |K| = 4 idx2 |1-omega| / omega (0: test unavailable)
   // Rayleigh-Benard (runs as case CAVITY with the lid at rest, plus T)
   double kappa, buoy, t_hot, t_cold, t_ref;
 };
@@ -60,7 +61,7 @@ struct Coef {
 // Control block for one Poisson solve (device memory).
 struct PoissonCtl {
   double* ring;        // RING x RES_SHARDS x SHARD_STRIDE residual accumulators
-  const double* tol;   // [0] tolerance, [1] initial residual (set by tol_kernel)
+  const double* tol;   // [0] tolerance, [1] initial residual, [2] max|source| (set by tol_kernel)
   int* stop;           // [0] converged flag, [1] iteration count at convergence
   int check_every;
 };
@@ -463,6 +464,7 @@ __global__ void tol_kernel(Coef c, const double* __restrict__ srcmax, double* __
   if (threadIdx.x != 0) return;
   double m = 0.0;
   for (int k = 0; k < RES_SHARDS; ++k) m = fmax(m, srcmax[k * SHARD_STRIDE]);
+  tol[2] = m;  // max|f| over the interior: the proof-mode test's F
   if (c.case_id == CAVITY) {
     tol[0] = c.tol_factor * m;
     tol[1] = 1.0;
@@ -618,6 +620,7 @@ struct WaveCtx {
   double* pout;
   const double* f;
   int gi, gic, y0, y1, rmin, rmax;
+  int py0 = 0, py1 = 0;  // proof mode: rows [py0, py1) whose black cells prove (band rows, 1 <= j < ny)
   bool pair_ok, out_lane, icol_a, icol_b, open_a, open_b;
   __device__ bool fl_a(int j) const { return icol_a && j >= 1 && j <= g.ny && (open_a || j <= c.inlet_jmax); }
   __device__ bool fl_b(int j) const { return icol_b && j >= 1 && j <= g.ny && (open_b || j <= c.inlet_jmax); }
@@ -773,7 +776,8 @@ __device__ __forceinline__ double wave_march_ring(const Geo& g, const Coef& c, c
 
 // Convergence test of the residual recorded for iteration kk (launch-start
 // test of the reference's while condition, cavity-01.cpp:633): true = go on.
-__device__ __forceinline__ bool pair_go_on(const PoissonCtl& ctl, int kk, int lane, double tol) {
+// proof: the slot holds the proof ratio of iteration kk (go on iff > 1)
+__device__ __forceinline__ bool pair_go_on(const PoissonCtl& ctl, int kk, int lane, double tol, bool proof = false) {
   double prev;
   if (kk == 0) {
     prev = ctl.tol[1];
@@ -781,6 +785,7 @@ __device__ __forceinline__ bool pair_go_on(const PoissonCtl& ctl, int kk, int la
     const double* slot = ctl.ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
     prev = (lane < RES_SHARDS) ? slot[lane * SHARD_STRIDE] : 0.0;
     prev = wave_max(prev);
+    if (proof) return prev > 1.0;
   }
   return prev > tol;
 }
@@ -790,15 +795,19 @@ __device__ __forceinline__ bool pair_go_on(const PoissonCtl& ctl, int kk, int la
 // 0 = the initial residual; others only on check_every multiples): the first
 // one that meets the tolerance ends the solve there. Returns false if this
 // launch has nothing to do (stopped now or earlier). All waves agree.
-__device__ __forceinline__ bool window_go_on(const PoissonCtl& ctl, int ka, int kb, int lane, bool first_wave) {
+// proof (the tested launch ran in proof mode): an iteration the proof does not
+// settle ends the proof-mode launches there (stop code 2); the host evaluates
+// it exactly.
+__device__ __forceinline__ bool window_go_on(const PoissonCtl& ctl, int ka, int kb, int lane, bool first_wave,
+                                             bool proof = false) {
   if (ctl.stop[0] != 0) return false;
   const double tol = ctl.tol[0];
   for (int kk = ka; kk <= kb; ++kk) {
     if (!(kk == 0 || (kk >= 1 && kk % ctl.check_every == 0))) continue;
-    if (!pair_go_on(ctl, kk, lane, tol)) {
+    if (!pair_go_on(ctl, kk, lane, tol, proof)) {
       if (first_wave && lane == 0) {
         ctl.stop[1] = kk;
-        ctl.stop[0] = 1;
+        ctl.stop[0] = (proof && kk > 0) ? 2 : 1;
       }
       return false;
     }
@@ -815,7 +824,7 @@ __global__ __launch_bounds__(256, CFD_WAVE_MIN_WAVES) void poisson_wave_kernel(G
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // convergence test of the iterations [ka, kb] (flags bit 2: none - a replay
   // of an iteration already known to be the solve's last)
-  if (!(flags & 4) && !window_go_on(ctl, ka, kb, lane, blockIdx.x == 0 && wv == 0)) return;
+  if (!(flags & 4) && !window_go_on(ctl, ka, kb, lane, blockIdx.x == 0 && wv == 0, (flags & 128) != 0)) return;
 
   if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS)
     ctl.ring[(size_t)((k + 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
@@ -1141,16 +1150,50 @@ struct CavRun {
   double2 fr[10];    // source rows R-d .. R-10d
   double2 np[5];     // prefetched p_in rows R .. R+4d
   double2 nf[5];     // prefetched f rows R-d .. R+3d
-  double rmax[NS];
+  double rmax[NS];   // exact mode: max |residual| per sweep; proof mode: max |black update| per sweep
+  double pm;         // proof mode: max |p_out| over the cells this wave stores
 };
+
+// ---------------------------------------------- proof-mode convergence test --
+//
+// The reference keeps sweeping while max|r| > tol (cavity-01.cpp:633, the
+// residual of :659-677). To go on it is enough that ONE cell has |r| > tol.
+// For a black cell with four neighbours (1 < i < nx, 1 <= j < ny) the
+// residual right after its update follows from the update itself: with
+// p' = (1-w) p + (w/4) (S - h^2 f) and r = idx2 (S - 4 p') - f,
+//     r = K (p' - p) + E,   K = 4 idx2 (1-w)/w,
+// where |E| is bounded by the rounding of the update and of the residual's
+// own evaluation: |E| + |r_ref - r| <= 128 u idx2 P + 16 u F (u = 2^-53, P a
+// bound on every |p| in the cell's stencil, F on |f|; DESIGN.md §2 has the
+// derivation; requires 0.5 <= w < 2). Each sweep grows max|p| by at most 9x
+// (red then black, w < 2) plus h^2 F, so over a launch P <= 9^NS (Pin + h^2 F),
+// Pin = max|p_in| (every launch records max|p_out|; the solve starts from
+// zero) and F = max|f| over the interior (tolerance pass). Hence
+//     |p' - p| > thr = (tol + 2^-43 (idx2 P + F)) / |K|  (x (1 + 2^-38))
+// proves |r_ref| > tol, i.e. the reference's loop goes on, with the computed
+// fields untouched. The wave records max|p' - p| / thr per sweep (> 1:
+// proven). A sweep that is not proven this way (only near convergence, or
+// with non-finite values) is evaluated exactly: the host reruns the launch
+// that computed it with the exact residual kernel and finishes the solve so.
+__device__ __forceinline__ double proof_ratio(const Coef& c, double tol, double dmax, double pin, double fmx,
+                                              double growth) {
+  // (a NaN bound fails every comparison below: q = 0)
+  const double P = growth * (pin + c.h2 * fmx) * (1.0 + 0x1p-40);
+  const double margin = 0x1p-43 * (c.idx2 * P + fmx);
+  const double thr = (tol + margin) / c.proof_k * (1.0 + 0x1p-38);
+  const double q = dmax / thr;
+  return (q == q && q >= 0.0) ? q : 0.0;  // non-finite bounds prove nothing
+}
 
 // slot of row R - X d in a 10-slot ring at step t = (ROT, PAR) of the 10-step march
 #define CFD_S10(X) ((((6 * (ROT) + 5 * (PAR)) % 10 + 9 - (X)) % 10 + 20) % 10)
 
-// red (COLOR 0) / black (COLOR 1) update of row j = R - X d (parity JPAR)
-template <int DIR, int ROT, int JPAR, int COLOR, bool EDGE>
+// red (COLOR 0) / black (COLOR 1) update of row j = R - X d (parity JPAR).
+// PROOF (interior waves): the black update also records |p' - p| x wgt
+// (wgt = 1 on rows whose cells prove, 0 elsewhere: a row-uniform scalar).
+template <int DIR, int ROT, int JPAR, int COLOR, bool EDGE, bool PROOF = false>
 __device__ __forceinline__ void cav_update(const WaveCtx<CAVITY>& x, double2 (&W)[5], int j, int X,
-                                           const double2& fc) {
+                                           const double2& fc, double wgt = 0.0, double* dm = nullptr) {
   double2& m = W[CFD_SLOT(X)];
   const double2 bh = W[CFD_SLOT(X + 1)], ah = W[CFD_SLOT(X - 1)];
 #define CFD_S(b, a) ((DIR > 0) ? (b) : (a))
@@ -1163,7 +1206,9 @@ __device__ __forceinline__ void cav_update(const WaveCtx<CAVITY>& x, double2 (&W
                                              CFD_N(bh.x, ah.x), fc.x);
         m.x = x.fl_a(j) ? nv : m.x;
       } else {
+        const double old = m.x;
         m.x = sor_fast<CAVITY>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+        if (PROOF && COLOR == 1) *dm = fmax(*dm, fabs(m.x - old) * wgt);
       }
     } else {
       const double Ra = dpp_from_right(m.x);
@@ -1172,7 +1217,9 @@ __device__ __forceinline__ void cav_update(const WaveCtx<CAVITY>& x, double2 (&W
                                              CFD_N(bh.y, ah.y), fc.y);
         m.y = x.fl_b(j) ? nv : m.y;
       } else {
+        const double old = m.y;
         m.y = sor_fast<CAVITY>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+        if (PROOF && COLOR == 1) *dm = fmax(*dm, fabs(m.y - old) * wgt);
       }
     }
   }
@@ -1180,13 +1227,24 @@ __device__ __forceinline__ void cav_update(const WaveCtx<CAVITY>& x, double2 (&W
 #undef CFD_N
 }
 
-template <int DIR, int ROT, bool EDGE>
+template <int DIR, int ROT, bool EDGE, bool PROOF = false>
 __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const double2 (&W)[5], int j, int X,
                                              const double2& fc, bool store, double& rm) {
   const int nx = x.g.nx, ny = x.g.ny;
   const Coef& c = x.c;
 #define CFD_S(b, a) ((DIR > 0) ? (b) : (a))
 #define CFD_N(b, a) ((DIR > 0) ? (a) : (b))
+  if (PROOF) {  // no residual: the store of the last sweep, and max|p_out| (in rm)
+    if (store && j >= x.y0 && j < x.y1 && x.out_lane) {
+      const double2 m = W[CFD_SLOT(X)];
+      rm = fmax(rm, fmax(fabs(m.x), fabs(m.y)));
+      double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      d2v mv = {m.x, m.y};
+      __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
+    }
+    return;
+  }
   if (j >= x.y0 && j < x.y1) {  // row-uniform
     const double2 m = W[CFD_SLOT(X)], bh = W[CFD_SLOT(X + 1)], ah = W[CFD_SLOT(X - 1)];
     const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
@@ -1222,20 +1280,26 @@ __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const dou
 }
 
 // sweeps S .. NS-1 of one march step (compile-time recursion over the sweeps)
-template <int S, int NS, int DIR, int ROT, int PAR, bool EDGE>
+template <int S, int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF>
 __device__ __forceinline__ void cav_sweeps(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R) {
   if constexpr (S < NS) {
     // red at R-(2S+1)d (parity PAR^1), black at R-(2S+2)d (PAR), residual at R-(2S+3)d
     cav_update<DIR, ROT, PAR ^ 1, 0, EDGE>(x, s.w[S], R - (2 * S + 1) * DIR, 2 * S + 1, s.fr[CFD_S10(2 * S + 1)]);
-    cav_update<DIR, ROT, PAR, 1, EDGE>(x, s.w[S], R - (2 * S + 2) * DIR, 2 * S + 2, s.fr[CFD_S10(2 * S + 2)]);
-    cav_residual<DIR, ROT, EDGE>(x, s.w[S], R - (2 * S + 3) * DIR, 2 * S + 3, s.fr[CFD_S10(2 * S + 3)], S == NS - 1,
-                                 s.rmax[S]);
+    if constexpr (PROOF && !EDGE) {
+      const int jb = R - (2 * S + 2) * DIR;
+      const double wgt = (jb >= x.py0 && jb < x.py1) ? 1.0 : 0.0;  // row-uniform
+      cav_update<DIR, ROT, PAR, 1, EDGE, true>(x, s.w[S], jb, 2 * S + 2, s.fr[CFD_S10(2 * S + 2)], wgt, &s.rmax[S]);
+    } else {
+      cav_update<DIR, ROT, PAR, 1, EDGE>(x, s.w[S], R - (2 * S + 2) * DIR, 2 * S + 2, s.fr[CFD_S10(2 * S + 2)]);
+    }
+    cav_residual<DIR, ROT, EDGE, PROOF>(x, s.w[S], R - (2 * S + 3) * DIR, 2 * S + 3, s.fr[CFD_S10(2 * S + 3)],
+                                        S == NS - 1, PROOF ? s.pm : s.rmax[S]);
     if constexpr (S + 1 < NS) s.w[S + 1][CFD_SLOT(2 * S + 2)] = s.w[S][CFD_SLOT(2 * S + 2)];
-    cav_sweeps<S + 1, NS, DIR, ROT, PAR, EDGE>(x, s, R);
+    cav_sweeps<S + 1, NS, DIR, ROT, PAR, EDGE, PROOF>(x, s, R);
   }
 }
 
-template <int NS, int DIR, int ROT, int PAR, bool EDGE>  // PAR = parity of R
+template <int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF>  // PAR = parity of R
 __device__ __forceinline__ void cav_step(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R) {
   s.w[0][CFD_SLOT(0)] = s.np[CFD_SLOT(0)];
   s.fr[CFD_S10(1)] = s.nf[CFD_SLOT(0)];
@@ -1246,11 +1310,14 @@ __device__ __forceinline__ void cav_step(const WaveCtx<CAVITY>& x, CavRun<NS>& s
     s.np[CFD_SLOT(-4)] = x.ld_fast(x.pin, R + 4 * DIR);
     s.nf[CFD_SLOT(-4)] = x.ld_fast(x.f, R + 3 * DIR);
   }
-  cav_sweeps<0, NS, DIR, ROT, PAR, EDGE>(x, s, R);
+  cav_sweeps<0, NS, DIR, ROT, PAR, EDGE, PROOF>(x, s, R);
 }
 
-template <int NS, int DIR, bool EDGE>
-__device__ __forceinline__ void cav_march(const WaveCtx<CAVITY>& x, int y0, int y1, double (&r)[NS]) {
+// PROOF: r[q] = max |black update| of sweep q over the output cells
+// (interior waves; 0 on boundary-column waves), pm = max |p_out| stored
+template <int NS, int DIR, bool EDGE, bool PROOF = false>
+__device__ __forceinline__ void cav_march(const WaveCtx<CAVITY>& x, int y0, int y1, double (&r)[NS],
+                                          double* pm = nullptr) {
   constexpr int H = 2 * NS + 1;
   const int Rb0 = (DIR > 0) ? y0 - H : y1 - 1 + H;
   const int Rbeg = Rb0 - DIR * (Rb0 & 1);  // even first front row: compile-time colours
@@ -1265,6 +1332,7 @@ __device__ __forceinline__ void cav_march(const WaveCtx<CAVITY>& x, int y0, int 
   for (int k = 0; k < 10; ++k) s.fr[k] = z;
 #pragma unroll
   for (int q = 0; q < NS; ++q) s.rmax[q] = 0.0;
+  s.pm = 0.0;
   {
     constexpr int ROT = 0;
 #pragma unroll
@@ -1275,19 +1343,25 @@ __device__ __forceinline__ void cav_march(const WaveCtx<CAVITY>& x, int y0, int 
   }
   int R = Rbeg;
   for (int st = 0; st < nsteps; st += 10, R += 10 * DIR) {
-    cav_step<NS, DIR, 0, 0, EDGE>(x, s, R);
-    cav_step<NS, DIR, 1, 1, EDGE>(x, s, R + DIR);
-    cav_step<NS, DIR, 2, 0, EDGE>(x, s, R + 2 * DIR);
-    cav_step<NS, DIR, 3, 1, EDGE>(x, s, R + 3 * DIR);
-    cav_step<NS, DIR, 4, 0, EDGE>(x, s, R + 4 * DIR);
-    cav_step<NS, DIR, 0, 1, EDGE>(x, s, R + 5 * DIR);
-    cav_step<NS, DIR, 1, 0, EDGE>(x, s, R + 6 * DIR);
-    cav_step<NS, DIR, 2, 1, EDGE>(x, s, R + 7 * DIR);
-    cav_step<NS, DIR, 3, 0, EDGE>(x, s, R + 8 * DIR);
-    cav_step<NS, DIR, 4, 1, EDGE>(x, s, R + 9 * DIR);
+    cav_step<NS, DIR, 0, 0, EDGE, PROOF>(x, s, R);
+    cav_step<NS, DIR, 1, 1, EDGE, PROOF>(x, s, R + DIR);
+    cav_step<NS, DIR, 2, 0, EDGE, PROOF>(x, s, R + 2 * DIR);
+    cav_step<NS, DIR, 3, 1, EDGE, PROOF>(x, s, R + 3 * DIR);
+    cav_step<NS, DIR, 4, 0, EDGE, PROOF>(x, s, R + 4 * DIR);
+    cav_step<NS, DIR, 0, 1, EDGE, PROOF>(x, s, R + 5 * DIR);
+    cav_step<NS, DIR, 1, 0, EDGE, PROOF>(x, s, R + 6 * DIR);
+    cav_step<NS, DIR, 2, 1, EDGE, PROOF>(x, s, R + 7 * DIR);
+    cav_step<NS, DIR, 3, 0, EDGE, PROOF>(x, s, R + 8 * DIR);
+    cav_step<NS, DIR, 4, 1, EDGE, PROOF>(x, s, R + 9 * DIR);
   }
+  if constexpr (PROOF) {
+    *pm = s.pm;
 #pragma unroll
-  for (int q = 0; q < NS; ++q) r[q] = (EDGE || x.out_lane) ? s.rmax[q] : 0.0;
+    for (int q = 0; q < NS; ++q) r[q] = (!EDGE && x.out_lane) ? s.rmax[q] : 0.0;
+  } else {
+#pragma unroll
+    for (int q = 0; q < NS; ++q) r[q] = (EDGE || x.out_lane) ? s.rmax[q] : 0.0;
+  }
 }
 #undef CFD_S10
 
@@ -1352,12 +1426,17 @@ struct PairPlan {
   int lo0, hi0, lo1, hi1;
 };
 
-template <int CASE, int NS>
+// PROOF (cavity): the convergence test of each sweep is the proof above
+// instead of the max-norm residual; the fields are the same bits.
+template <int CASE, int NS, bool PROOF = false>
 __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAIR_MIN_WAVES) void poisson_multi_kernel(
     Geo g, Coef c, const double* __restrict__ pin, double* __restrict__ pout, const double* __restrict__ f,
     PoissonCtl ctl, int k, int ka, int kb, PairPlan pl, int flags) {
   // NS red-black iterations k .. k+NS-1 in one launch (NS = 3: cavity only)
-  static_assert(NS == 2 || (NS == 3 && CASE == CAVITY), "three sweeps per launch: cavity pipeline only");
+  // (NS = 4: proof mode only - without the residual stage its dependency depth
+  // is 2 NS = 8 rows / columns, the stored halo)
+  static_assert(NS == 2 || (NS == 3 && CASE == CAVITY) || (NS == 4 && PROOF), "sweeps per launch");
+  static_assert(!PROOF || CASE == CAVITY, "proof-mode test: cavity pipeline only");
   // tiles: the first and last column tile (boundary columns, general masks)
   // in bands of pl.the rows, then the interior column tiles in bands of pl.th
   // rows; the host makes the boundary bands shorter so that their slower
@@ -1367,11 +1446,12 @@ __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAI
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: band / row logic stays scalar
 
   // convergence test of the iterations [ka, kb] (flags bit 2: none, a replay)
-  if (!(flags & 4) && !window_go_on(ctl, ka, kb, lane, blockIdx.x == 0 && wv == 0)) return;
+  if (!(flags & 4) && !window_go_on(ctl, ka, kb, lane, blockIdx.x == 0 && wv == 0, (flags & 128) != 0)) return;
   if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS) {  // the next launch's residual slots
 #pragma unroll
     for (int q = 0; q < NS; ++q)
       ctl.ring[(size_t)((k + NS + q) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
+    if (PROOF && lane == 0) ctl.ring[(size_t)((k + NS) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + 1] = 0.0;
   }
 
   const int nblk = (int)gridDim.x;
@@ -1436,12 +1516,40 @@ __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAI
   }
   const bool up = (flags & 1) && (band & 1);
   // flags bit 4 / bit 5 (timing diagnostics only): never / always take the interior path
-  const bool fast = (flags & 32) || (!(flags & 16) && cols_in);
+  // (the proof needs four-neighbour cells: never forced onto the interior path)
+  const bool fast = PROOF ? cols_in : ((flags & 32) || (!(flags & 16) && cols_in));
   double r[NS];
   if constexpr (CASE == CAVITY) {  // the cavity's own pipeline (no refresh stage: depth 2NS+1)
-    if (!fast) cav_march<NS, 1, true>(x, y0, y1, r);
-    else if (up) cav_march<NS, -1, false>(x, y0, y1, r);
-    else cav_march<NS, 1, false>(x, y0, y1, r);
+    if constexpr (PROOF) {
+      x.py0 = max(y0, 1);
+      x.py1 = min(y1, g.ny);
+      double pm = 0.0;
+      if (!fast) cav_march<NS, 1, true, true>(x, y0, y1, r, &pm);
+      else if (up) cav_march<NS, -1, false, true>(x, y0, y1, r, &pm);
+      else cav_march<NS, 1, false, true>(x, y0, y1, r, &pm);
+      // P bound of this launch: max|p_out| of the launch before (ring slot of
+      // its first iteration, element 1), or with the lagged test (ranks; that
+      // one's maximum may not be all-reduced yet) of the launch before that,
+      // grown over one more launch; none before the first launch (the solve
+      // starts from a zero field)
+      const bool lag = (flags & 256) != 0;
+      const int kp = k - (lag ? 2 * NS : NS);
+      double pin = (kp >= 1) ? ctl.ring[(size_t)(kp & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + 1] : 0.0;
+      constexpr double growth = (NS == 2) ? 81.0 : (NS == 3) ? 729.0 : 6561.0;
+      const double F = ctl.tol[2];
+      if (lag) pin = growth * (pin + c.h2 * F) * (1.0 + 0x1p-40);
+      const double tol = ctl.tol[0];
+      pm = wave_max(pm);
+#pragma unroll
+      for (int q = 0; q < NS; ++q) r[q] = proof_ratio(c, tol, wave_max(r[q]), pin, F, growth);
+      if (lane == 0 && pm > 0.0)  // this launch's max|p_out| (zeroed by the launch before)
+        atomicMax(reinterpret_cast<unsigned long long*>(ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + 1),
+                  (unsigned long long)__double_as_longlong(pm));
+    } else {
+      if (!fast) cav_march<NS, 1, true>(x, y0, y1, r);
+      else if (up) cav_march<NS, -1, false>(x, y0, y1, r);
+      else cav_march<NS, 1, false>(x, y0, y1, r);
+    }
   } else {
     double r1 = 0.0, r2 = 0.0;
     if (fast) {

@@ -78,6 +78,11 @@ static Coef make_coef(const cfd_params& p) {
   c.open_cv = p.dt / (p.rho * p.dy);
   c.tol_factor = p.tol_factor;
   c.abs_tol = p.abs_tol;
+  // proof-mode test (kernels.hpp, proof_ratio): its error bound assumes
+  // 1 - omega and omega / 4 exact, i.e. 0.5 <= omega <= 2
+  c.proof_k = (p.omega >= 0.5 && p.omega < 2.0 && p.omega != 1.0)
+                  ? 4.0 * c.idx2 * std::fabs(1.0 - p.omega) / p.omega
+                  : 0.0;
   c.kappa = p.kappa;
   c.buoy = p.buoyancy;
   c.t_hot = p.t_hot;
@@ -125,14 +130,28 @@ class Solver {
     return P.case_id == CFD_CAVITY ? 3 : 2;
   }
   struct LaunchRec {
-    int first, n;  // iterations first .. first+n-1
+    int first, n;        // iterations first .. first+n-1
+    bool proof = false;  // its ring slots hold proof ratios (proof-mode launch), not residuals
   };
+  // Proof-mode convergence test (kernels.hpp, proof_ratio): cavity 3-sweep
+  // launches prove "the reference goes on" from the black updates instead of
+  // evaluating the residual; an iteration it leaves open is evaluated exactly
+  // (the solve falls back to exact launches from the launch that computed it).
+  bool proof_launch = false;  // the launch being enqueued runs in proof mode
+  bool window_proof = false;  // the window it tests was computed in proof mode
+  bool proof_enabled = true;  // CFD_PROOF=0: exact residuals throughout
+  int proof_ns = 3;           // sweeps per proof-mode launch (3 or 4: CFD_PROOF_NS)
+  bool proof_ok() const {
+    // (only interior column tiles prove: at least one between the two boundary tiles)
+    return proof_enabled && P.case_id == CFD_CAVITY && sweeps_per_launch() == 3 && C.proof_k > 0.0 &&
+           (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC >= 3;
+  }
   std::vector<LaunchRec> launches;  // SOR launches of the current solve
   LaunchRec ar_pending{0, 0};       // overlapped launch whose residual all-reduce is not enqueued yet
 
   // enqueue the pending (lagged) all-reduce of an overlapped launch on xs
   void flush_allreduce(hipStream_t xs) {
-    if (ar_pending.n > 0) allreduce_slots(ar_pending.first, ar_pending.n, xs);
+    if (ar_pending.n > 0) allreduce_slots(ar_pending.first, ar_pending.n, xs, ar_pending.proof);
     ar_pending = {0, 0};
   }
   int nbufs() const { return lagged() ? 3 : 2; }
@@ -216,6 +235,8 @@ class Solver {
       if (const char* e = std::getenv("CFD_MARCH_MIN_TH")) march_min_th = std::max(1, std::atoi(e));  // tuning
       resident_pair_waves = pps * 4 * prop.multiProcessorCount;
     }
+    if (const char* e = std::getenv("CFD_PROOF")) proof_enabled = std::atoi(e) != 0;  // 0: exact residuals throughout
+    if (const char* e = std::getenv("CFD_PROOF_NS")) proof_ns = std::atoi(e) == 4 ? 4 : 3;
     pitch = ((P.nx + 3) + 15) / 16 * 16;  // >= nx+3: column pairs (gi, gi+1) stay inside a row
     size_t part = 0;
     for (auto [j0, j1] : rows) {
@@ -246,13 +267,13 @@ class Solver {
     HIPC(hipMalloc(&ring, ringn * sizeof(double)));
     HIPC(hipMalloc(&srcmax, RES_SHARDS * SHARD_STRIDE * sizeof(double)));
     HIPC(hipMalloc(&divmax, RES_SHARDS * SHARD_STRIDE * sizeof(double)));
-    HIPC(hipMalloc(&tolv, 2 * sizeof(double)));
+    HIPC(hipMalloc(&tolv, 4 * sizeof(double)));
     HIPC(hipMalloc(&total, 4 * sizeof(double)));
     HIPC(hipMalloc(&partials, std::max<size_t>(npart, 1) * sizeof(double)));
     HIPC(hipMalloc(&stop, 2 * sizeof(int)));
     HIPC(hipMalloc(&resmax, RES_SHARDS * SHARD_STRIDE * sizeof(double)));
     HIPC(hipMemsetAsync(ring, 0, ringn * sizeof(double), st));
-    HIPC(hipMemsetAsync(tolv, 0, 2 * sizeof(double), st));
+    HIPC(hipMemsetAsync(tolv, 0, 4 * sizeof(double), st));
     HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
     HIPC(hipHostMalloc(&h_stat, 4 * sizeof(int), hipHostMallocDefault));
     HIPC(hipHostMalloc(&h_shard, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipHostMallocDefault));
@@ -565,14 +586,25 @@ class Solver {
   template <int CASE>
   void launch_multi(int n, const PairPlan& pl, const Geo& g, const double* pin, double* pout, const double* f,
                     const PoissonCtl& ctl, int k, int ka, int kb, hipStream_t stream, bool replay = false) {
-    const int fl = march_flags | (replay ? 4 : 0);  // bit 2: no test at all (the solve has already stopped)
+    // bit 2: no test at all (the solve has already stopped); bit 7: the tested
+    // window holds proof ratios (it was computed by a proof-mode launch)
+    // bit 8: proof-mode P bound from the launch before the previous one (lagged test)
+    const int fl = march_flags | (replay ? 4 : 0) | (window_proof ? 128 : 0) | (lagged() ? 256 : 0);
     const int ne = pl.ctiles >= 2 ? 2 : 1;
     const int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
     if (ntiles == 0) return;
     const dim3 grid((ntiles + 3) / 4);
     if constexpr (CASE == CAVITY) {
+      if (n == 4) {  // proof mode only (Solver::proof_ns)
+        if (!proof_launch || replay) throw Error(CFD_E_STATE, "four sweeps per launch: proof mode only");
+        poisson_multi_kernel<CASE, 4, true><<<grid, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, ka, kb, pl, fl);
+        return;
+      }
       if (n == 3) {
-        poisson_multi_kernel<CASE, 3><<<grid, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, ka, kb, pl, fl);
+        if (proof_launch && !replay)
+          poisson_multi_kernel<CASE, 3, true><<<grid, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, ka, kb, pl, fl);
+        else
+          poisson_multi_kernel<CASE, 3><<<grid, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, ka, kb, pl, fl);
         return;
       }
     }
@@ -594,7 +626,7 @@ class Solver {
         wave_bands(rows, 128 - 8, resident_waves, ctiles, th, nbands);
         const int nblk = (ctiles * nbands + 3) / 4;
         poisson_wave_kernel<CASE><<<nblk, 256, 0, st>>>(g, C, pin[q], pout[q], S[q].b[B_F], ctl, k, ka, kb, th, ctiles,
-                                                         nbands, march_flags | (replay ? 4 : 0));
+                                                         nbands, march_flags | (replay ? 4 : 0) | (window_proof ? 128 : 0));
       }
     }
     check_launch("poisson");
@@ -610,7 +642,8 @@ class Solver {
 
   // all-reduce (max) of the residual slots of iterations k .. k+n-1 that are tested
   // (slots adjacent in the ring go in one call: one RCCL latency per launch)
-  void allreduce_slots(int k, int n, hipStream_t xs) {
+  // (a proof-mode launch: its first slot also holds its max|p_out|, always reduced)
+  void allreduce_slots(int k, int n, hipStream_t xs, bool proof) {
     constexpr size_t SLOT = (size_t)RES_SHARDS * SHARD_STRIDE;
     int run0 = -1, runn = 0;  // ring slots [run0, run0 + runn) pending
     auto flush = [&] {
@@ -618,7 +651,7 @@ class Solver {
       runn = 0;
     };
     for (int kk = k; kk < k + n && kk <= P.max_iters; ++kk) {
-      if (!(kk % P.check_every == 0 || kk == P.max_iters)) continue;
+      if (!(kk % P.check_every == 0 || kk == P.max_iters || (proof && kk == k))) continue;
       const int sl = kk & (RING - 1);
       if (runn > 0 && sl == run0 + runn) {
         ++runn;
@@ -671,7 +704,7 @@ class Solver {
     check_launch("poisson (overlapped)");
     HIPC(hipEventRecord(ev_int[e], st));
     HIPC(hipEventRecord(ev_bnd[e], st_b));
-    ar_pending = {k, n};
+    ar_pending = {k, n, proof_launch};
     last_bnd = e;
     b_pending = true;
     ++n_overlapped;
@@ -702,7 +735,7 @@ class Solver {
     if (P.case_id == CFD_CAVITY) launch_poisson<CAVITY>(pin.data(), pout.data(), k, n, ka, kb, replay);
     else if (P.case_id == CFD_CHANNEL) launch_poisson<CHANNEL>(pin.data(), pout.data(), k, n, ka, kb, replay);
     else launch_poisson<BACKSTEP>(pin.data(), pout.data(), k, n, ka, kb, replay);
-    if (comm && comm->nranks > 1 && !replay) allreduce_slots(k, n, st);
+    if (comm && comm->nranks > 1 && !replay) allreduce_slots(k, n, st, proof_launch);
   }
 
   // solverPressurePoisson (cavity-01.cpp:609-690, channel-01.cpp:635-688,
@@ -1031,6 +1064,22 @@ class Solver {
     }
   }
 
+  // max-norm residual of the cavity field in p buffer `bp` (cavity-01.cpp:659-677)
+  double final_residual(int bp) {
+    if (multi()) exchange(bp, 1);
+    HIPC(hipMemsetAsync(resmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
+    for (auto& s : S) {
+      cavity_resmax_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_F], resmax);
+      check_launch("cavity_resmax");
+    }
+    if (comm && comm->nranks > 1) comm_allreduce_max(comm, resmax, RES_SHARDS * SHARD_STRIDE, st);
+    HIPC(hipMemcpyAsync(h_shard, resmax, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    double res = 0.0;
+    for (int q = 0; q < RES_SHARDS; ++q) res = std::max(res, h_shard[q * SHARD_STRIDE]);
+    return res;
+  }
+
   void solve(cfd_step_info* out) {
     if (use_lexw()) {
       solve_lexw(out);
@@ -1066,69 +1115,115 @@ class Solver {
     HIPC(hipEventRecord(ev_a, st));
     int k = 0, c = 0, m = 0;
     int last_tested = -1;  // highest iteration some launch tests
-    bool stopped = false;
-    while (k < P.max_iters && !stopped) {
-      for (int j = 0; j < chunk && k < P.max_iters; ++j, ++m) {
-        const int n = std::min(spl, P.max_iters - k);
-        const int src = m - 1 - lag;
-        int ka = 1, kb = 0;  // empty window
-        if (src >= 0) {
-          ka = launches[src].first;
-          kb = ka + launches[src].n - 1;
-        } else if (src == -1) {
-          ka = kb = 0;
+    // Proof mode (cavity 3/4-sweep launches): windows test proof ratios. An
+    // iteration the proof leaves open restarts the solve at the launch that
+    // computed it (its input is intact: later launches exited at entry), with
+    // exact launches for one chunk, then proof mode again; windows over the
+    // launches before it are empty (every one of their iterations was proven
+    // to go on). Each launch record says which kind of value its slots hold.
+    int proof_from = proof_ok() ? 0 : INT32_MAX;  // first launch (index) in proof mode
+    int exact_from = 0;  // first launch whose iterations later launches test
+    int iters = 0;
+    auto launch_of = [&](int kk) {
+      for (size_t q = 0; q < launches.size(); ++q)
+        if (kk >= launches[q].first && kk <= launches[q].first + launches[q].n - 1) return (int)q;
+      throw Error(CFD_E_STATE, "iteration outside the launches of this solve");
+    };
+    for (;;) {
+      bool stopped = false;
+      while (k < P.max_iters && !stopped) {
+        for (int j = 0; j < chunk && k < P.max_iters; ++j, ++m) {
+          const bool proof = m >= proof_from;
+          const int n = std::min(proof ? proof_ns : spl, P.max_iters - k);
+          const int src = m - 1 - lag;
+          int ka = 1, kb = 0;  // empty window
+          window_proof = false;
+          if (src >= exact_from) {
+            ka = launches[src].first;
+            kb = ka + launches[src].n - 1;
+            window_proof = launches[src].proof;
+          } else if (src == -1) {
+            ka = kb = 0;
+          }
+          proof_launch = proof && n >= 3;
+          poisson_launch(m, k + 1, n, base, ka, kb, false);
+          if (ka <= kb) last_tested = std::max(last_tested, kb);
+          launches.push_back({k + 1, n, proof_launch});
+          k += n;
         }
-        poisson_launch(m, k + 1, n, base, ka, kb, false);
-        if (ka <= kb) last_tested = std::max(last_tested, kb);
-        launches.push_back({k + 1, n});
-        k += n;
+        join_b();
+        HIPC(hipMemcpyAsync(h_stat + 2 * (c & 1), stop, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+        HIPC(hipEventRecord(ev_poll[c & 1], st));
+        if (c > 0) {
+          HIPC(hipEventSynchronize(ev_poll[(c - 1) & 1]));
+          if (h_stat[2 * ((c - 1) & 1)] != 0) stopped = true;
+        }
+        ++c;
       }
-      join_b();
-      HIPC(hipMemcpyAsync(h_stat + 2 * (c & 1), stop, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-      HIPC(hipEventRecord(ev_poll[c & 1], st));
+      flush_allreduce(st);  // overlapped launches all-reduce one launch late: the last one
+      int code = 0, kstop = 0;
       if (c > 0) {
         HIPC(hipEventSynchronize(ev_poll[(c - 1) & 1]));
-        if (h_stat[2 * ((c - 1) & 1)] != 0) stopped = true;
+        const int* hs = h_stat + 2 * ((c - 1) & 1);
+        code = hs[0];
+        kstop = hs[1];
       }
-      ++c;
+      iters = (code == 1) ? kstop : P.max_iters;
+      int open_k = (code == 2) ? kstop : -1;  // an iteration the proof left open
+      // iterations after the last one a launch tested (the last launch(es), and
+      // the initial residual if no launch tested it): tested here, in order (the
+      // reference's while condition, cavity-01.cpp:633)
+      if (code == 0 && last_tested < P.max_iters - 1) {
+        HIPC(hipStreamSynchronize(st));
+        double t2[2];
+        HIPC(hipMemcpy(t2, tolv, sizeof t2, hipMemcpyDeviceToHost));
+        for (int kk = last_tested + 1; kk <= P.max_iters - 1; ++kk) {
+          double r;
+          bool pr = false;
+          if (kk == 0) {
+            r = t2[1];
+          } else if (kk % P.check_every == 0) {
+            const double* slot = ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
+            HIPC(hipMemcpy(h_shard, slot, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost));
+            r = 0.0;
+            for (int q = 0; q < RES_SHARDS; ++q) r = std::max(r, h_shard[q * SHARD_STRIDE]);
+            pr = launches[launch_of(kk)].proof;
+          } else {
+            continue;
+          }
+          if (pr) {
+            if (!(r > 1.0)) {
+              open_k = kk;
+              break;
+            }
+          } else if (!(r > t2[0])) {
+            iters = kk;
+            break;
+          }
+        }
+      }
+      if (open_k < 0) break;
+      // exact evaluation from the launch that computed open_k
+      join_b();
+      HIPC(hipStreamSynchronize(st));
+      if (st_b) HIPC(hipStreamSynchronize(st_b));
+      const int L = launch_of(open_k);
+      k = launches[L].first - 1;
+      m = L;
+      launches.resize(L);
+      last_tested = k;
+      exact_from = L;
+      proof_from = L + chunk;
+      c = 0;  // the polls so far are stale (stop code 2): the next chunk starts a fresh sequence
+      ++T.proof_fallbacks;
+      HIPC(hipMemsetAsync(ring, 0, (size_t)RING * RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
+      HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
     }
-    flush_allreduce(st);  // overlapped launches all-reduce one launch late: the last one
+    proof_launch = window_proof = false;
     HIPC(hipEventRecord(ev_b, st));
-    int iters;
-    if (c > 0) {
-      HIPC(hipEventSynchronize(ev_poll[(c - 1) & 1]));
-      const int* hs = h_stat + 2 * ((c - 1) & 1);
-      iters = hs[0] ? hs[1] : P.max_iters;
-    } else {
-      iters = 0;
-    }
     HIPC(hipEventSynchronize(ev_b));
     float ms = 0.f;
     HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
-    // iterations after the last one a launch tested (the last launch(es), and
-    // the initial residual if no launch tested it): tested here, in order (the
-    // reference's while condition, cavity-01.cpp:633)
-    if (iters == P.max_iters && last_tested < P.max_iters - 1) {
-      double t2[2];
-      HIPC(hipMemcpy(t2, tolv, sizeof t2, hipMemcpyDeviceToHost));
-      for (int kk = last_tested + 1; kk <= P.max_iters - 1; ++kk) {
-        double r;
-        if (kk == 0) {
-          r = t2[1];
-        } else if (kk % P.check_every == 0) {
-          const double* slot = ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-          HIPC(hipMemcpy(h_shard, slot, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost));
-          r = 0.0;
-          for (int q = 0; q < RES_SHARDS; ++q) r = std::max(r, h_shard[q * SHARD_STRIDE]);
-        } else {
-          continue;
-        }
-        if (!(r > t2[0])) {
-          iters = kk;
-          break;
-        }
-      }
-    }
     // the launch that computed iteration `iters`; if it ran further, redo the
     // first r of its iterations from its (intact) input into its output buffer
     int last = -1, replayed = 0;
@@ -1167,6 +1262,10 @@ class Solver {
       double t2[2];
       HIPC(hipMemcpy(t2, tolv, sizeof t2, hipMemcpyDeviceToHost));
       res = t2[1];
+    } else if (launches[last].proof) {
+      // a proof-mode launch computed the last iteration (the cap): the
+      // reported residual is the final field's (cavity-01.cpp:659-677)
+      res = final_residual(pbuf((base + last + 1) % nbufs()));
     } else {
       const double* slot = ring + (size_t)(iters & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
       HIPC(hipMemcpy(h_shard, slot, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost));

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 5
+#define CFD_AMD_ABI_VERSION 6
 
 /* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
  * tree (only figures): it is the cavity's projection step with a resting lid
@@ -105,6 +105,8 @@ typedef struct cfd_timing {
   long long poisson_overlapped; /* pair launches split into interior + halo-overlapped boundary rows (ranks) */
   double poisson_steady_ms;   /* lexicographic order: device time of the launches with every cell active */
   long long poisson_steady_launches; /* (the ramps at the start / end of a solve excluded) */
+  long long proof_fallbacks;  /* red-black cavity: solves whose proof-mode convergence test left an
+                                 iteration open, finished with exact residuals */
 } cfd_timing;
 
 /* Library / ABI info. */

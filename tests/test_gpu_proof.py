@@ -1,0 +1,124 @@
+"""Proof-mode convergence test of the red-black cavity launches
+(kernels.hpp `proof_ratio`).
+
+The reference sweeps while max|r| > tol (cavity-01.cpp:633). A proof-mode
+launch does not evaluate the residual: it proves "some cell has |r| > tol"
+from the size of its black updates (r = K (p' - p) + rounding terms it
+bounds), and an iteration it cannot settle that way is evaluated exactly (the
+solve restarts, with the exact residual kernel, at the launch that computed
+it). The test must be invisible: the same iteration counts, the same reported
+residuals and the same fields, bit for bit, as exact residuals throughout
+(CFD_PROOF=0) and as the red-black oracle.
+"""
+from __future__ import annotations
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import cfd_amd as C  # noqa: E402
+import oracle as O  # noqa: E402
+from test_gpu_parity import assert_bits  # noqa: E402
+
+FIELDS = ("p", "u", "v")
+
+
+@pytest.fixture(autouse=True)
+def multi_launch_path(monkeypatch):
+    monkeypatch.setenv("CFD_SMALL", "0")  # the multi-launch solve, at any size
+
+
+def run(monkeypatch, cp, steps, proof, ns=3, last_timing=False, **kw):
+    """proof: the proof-mode test with `ns` sweeps per launch (3, or 4: no
+    residual stage, so four sweeps fit the 8-row halos); else exact residuals.
+    last_timing: timing of the last step only."""
+    monkeypatch.setenv("CFD_PROOF", "1" if proof else "0")
+    monkeypatch.setenv("CFD_PROOF_NS", str(ns))
+    g = C.CavitySolver(cp, device=0, **kw)
+    hist = []
+    for s in range(steps):
+        if last_timing and s == steps - 1:
+            g.reset_timing()
+        hist.append(g.step())
+    out = {n: g.field(n).copy() for n in FIELDS}
+    tm = g.timing()
+    g.close()
+    return hist, out, tm
+
+
+def same(a, b, what):
+    (h0, f0, _), (h1, f1, _) = a, b
+    assert h1 == h0, what
+    for n in FIELDS:
+        assert_bits(f1[n], f0[n], f"{what} {n}")
+
+
+@pytest.mark.parametrize("ns", [3, 4])
+@pytest.mark.parametrize("nx,ny", [(240, 200), (357, 290)])
+def test_converging_solves_fall_back_and_match_oracle(monkeypatch, nx, ny, ns):
+    """Solves that converge: the proof settles the early iterations, the last
+    ones near the tolerance are evaluated exactly (fallback), and the stop
+    lands on the reference's iteration."""
+    cp = C.make_params("cavity", nx=nx, ny=ny)
+    ex = run(monkeypatch, cp, 3, False)
+    pr = run(monkeypatch, cp, 3, True, ns)
+    same(ex, pr, f"proof ({ns} sweeps) vs exact {nx}x{ny}")
+    assert ex[2].proof_fallbacks == 0
+    converged = [k for k, _ in ex[0] if k < cp.max_iters]
+    assert converged, "fixture meant to converge"
+    assert pr[2].proof_fallbacks >= len(converged)
+    o = O.Oracle(cp, ordering=O.RB)
+    ho = [o.step() for _ in range(3)]
+    assert ho == ex[0]
+    assert_bits(pr[1]["p"], o.field("p"), "p vs oracle")
+
+
+@pytest.mark.parametrize("ns", [3, 4])
+@pytest.mark.parametrize("cap", [30, 31, 32, 33, 34, 35, 100])
+def test_capped_solves_never_fall_back(monkeypatch, cap, ns):
+    """Capped solves far from convergence (1024^2, BASELINE configs[1]): every
+    iteration proven, shorter last launches (n = 1, 2) test the proof ratios
+    of the launch before, the host tests the last ones; the reported residual
+    is recomputed from the final field and equals the exact launches' one.
+    (The first timestep's source lives in the two lid corners only, so its
+    first sweep moves no cell that can prove: one fallback there, by design;
+    the second step must need none.)"""
+    cp = C.make_params("cavity", nx=1024, ny=1024, max_iters=cap)
+    ex = run(monkeypatch, cp, 2, False)
+    pr = run(monkeypatch, cp, 2, True, ns, last_timing=True)
+    same(ex, pr, f"cap {cap}, {ns} sweeps")
+    assert pr[2].proof_fallbacks == 0
+    assert all(k == cap for k, _ in pr[0])
+
+
+@pytest.mark.parametrize("ns", [3, 4])
+@pytest.mark.parametrize("check_every", [1, 8])
+def test_strips_and_check_every(monkeypatch, check_every, ns):
+    cp = C.make_params("cavity", nx=300, ny=260)
+    ex = run(monkeypatch, cp, 2, False, check_every=check_every)
+    pr = run(monkeypatch, cp, 2, True, ns, check_every=check_every, n_strips=3)
+    same(ex, pr, f"3 strips, check_every {check_every}")
+
+
+@pytest.mark.parametrize("ns", [3, 4])
+@pytest.mark.parametrize("delta", [-4, -1, 0, 1, 2, 5])
+def test_cap_around_the_natural_stop(monkeypatch, delta, ns):
+    """Caps just below / at / above the converged iteration: the fallback and
+    the cap meet in every order."""
+    cp = C.make_params("cavity", nx=240, ny=200)
+    K = run(monkeypatch, cp, 1, False)[0][0][0]
+    assert K < cp.max_iters
+    cp2 = C.make_params("cavity", nx=240, ny=200, max_iters=K + delta)
+    same(run(monkeypatch, cp2, 1, False), run(monkeypatch, cp2, 1, True, ns), f"cap K{delta:+d}")
+
+
+@pytest.mark.parametrize("ns", [3, 4])
+def test_full_size_step_proven(monkeypatch, ns):
+    """The bench's grid (4096^2), 61 capped sweeps: after the first step (see
+    above) the proof settles every iteration, and the fields equal the exact
+    launches'."""
+    cp = C.make_params("cavity", nx=4096, ny=4096, max_iters=61)
+    ex = run(monkeypatch, cp, 2, False)
+    pr = run(monkeypatch, cp, 2, True, ns, last_timing=True)
+    same(ex, pr, f"4096^2, {ns} sweeps")
+    assert pr[2].proof_fallbacks == 0

@@ -44,7 +44,7 @@ def test_nm_exports_match_header():
 
 
 def test_abi_version():
-    assert _lib.lib().cfd_abi_version() == 5
+    assert _lib.lib().cfd_abi_version() == 6
 
 
 @pytest.mark.parametrize("case", ["cavity", "channel", "backwards_step"])
