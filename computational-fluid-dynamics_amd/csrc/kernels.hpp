@@ -621,6 +621,12 @@ struct WaveCtx {
   const double* f;
   int gi, gic, y0, y1, rmin, rmax;
   int py0 = 0, py1 = 0;  // proof mode: rows [py0, py1) whose black cells prove (band rows, 1 <= j < ny)
+  // cavity boundary-column waves: the reference's indicator products as lane
+  // constants (eps_e, eps_w as 1.0 / 0.0; x * 0.0 == copysign(0, x), the
+  // reference's 0 * x, for finite x) and omega / neighbour_count below / at
+  // the top row, per column slot (cav_edge_lanes)
+  double ce_a = 1.0, cw_a = 1.0, ce_b = 1.0, cw_b = 1.0;
+  double om_a = 0.0, om_at = 0.0, om_b = 0.0, om_bt = 0.0;
   bool pair_ok, out_lane, icol_a, icol_b, open_a, open_b;
   __device__ bool fl_a(int j) const { return icol_a && j >= 1 && j <= g.ny && (open_a || j <= c.inlet_jmax); }
   __device__ bool fl_b(int j) const { return icol_b && j >= 1 && j <= g.ny && (open_b || j <= c.inlet_jmax); }
@@ -1144,12 +1150,28 @@ __device__ __forceinline__ void wave_march_pair(const WaveCtx<CASE>& x, int y0, 
 // (sor_fast / residual_interior, rows by uniform branches); boundary-column
 // waves the reference's masked forms (sor_update / residual_abs).
 
+// cavity interior bands march alternately down / up (1), or all down (0)
+#ifndef CFD_CAV_UP
+#define CFD_CAV_UP 1
+#endif
+// rows of p_in / f in flight per cavity wave (prefetch distance, <= 9): exact
+// launches / proof-mode launches of 3 and 4 sweeps (as deep as 3 waves/SIMD allow)
+#ifndef CFD_CAV_PD
+#define CFD_CAV_PD 4
+#endif
+#ifndef CFD_CAV_PD3
+#define CFD_CAV_PD3 4
+#endif
+#ifndef CFD_CAV_PD4
+#define CFD_CAV_PD4 4
+#endif
+
 template <int NS>
 struct CavRun {
   double2 w[NS][5];  // sweep s: rows R-2s d .. R-(2s+4) d
   double2 fr[10];    // source rows R-d .. R-10d
-  double2 np[5];     // prefetched p_in rows R .. R+4d
-  double2 nf[5];     // prefetched f rows R-d .. R+3d
+  double2 np[10];    // prefetched p_in rows R .. R+PD d (row R - X d in slot CFD_S10(X))
+  double2 nf[10];    // prefetched f rows R-d .. R+(PD-1) d (same slots)
   double rmax[NS];   // exact mode: max |residual| per sweep; proof mode: max |black update| per sweep
   double pm;         // proof mode: max |p_out| over the cells this wave stores
 };
@@ -1188,37 +1210,75 @@ __device__ __forceinline__ double proof_ratio(const Coef& c, double tol, double 
 // slot of row R - X d in a 10-slot ring at step t = (ROT, PAR) of the 10-step march
 #define CFD_S10(X) ((((6 * (ROT) + 5 * (PAR)) % 10 + 9 - (X)) % 10 + 20) % 10)
 
+// the lane constants of a cavity boundary-column wave (columns gi, gi+1)
+__device__ __forceinline__ void cav_edge_lanes(WaveCtx<CAVITY>& x) {
+  const int nx = x.g.nx, ia = x.gi, ib = x.gi + 1;
+  x.ce_a = (ia < nx) ? 1.0 : 0.0;
+  x.cw_a = (ia > 1) ? 1.0 : 0.0;
+  x.ce_b = (ib < nx) ? 1.0 : 0.0;
+  x.cw_b = (ib > 1) ? 1.0 : 0.0;
+  const int na = (ia < nx) + (ia > 1) + 1, nb = (ib < nx) + (ib > 1) + 1;  // + eps_n (below the top row)
+  // om_nc[n] by value: a run-time index into Coef would copy it to scratch
+  double o1 = x.c.om_nc[1], o2 = x.c.om_nc[2], o3 = x.c.om_nc[3], o4 = x.c.om_nc[4];
+  auto pick = [&](int n) { return n == 4 ? o4 : n == 3 ? o3 : n == 2 ? o2 : o1; };
+  x.om_a = pick(na + 1);
+  x.om_at = pick(na);
+  x.om_b = pick(nb + 1);
+  x.om_bt = pick(nb);
+}
+
+// SOR update of a boundary-column wave's cell: sor_update<CAVITY> with the
+// indicators as lane constants (same operands, same order, same bits)
+__device__ __forceinline__ double cav_edge_sor(const Coef& c, bool top, double ce, double cw, double om, double omt,
+                                               double pc, double pW, double pE, double pS, double pN, double fc) {
+  const double tN = top ? pN * 0.0 : pN;  // row-uniform
+  return pc * c.one_m_omega + (top ? omt : om) * ((pE * ce + pW * cw) + (tN + pS) - fc * c.h2);
+}
+
+// |residual| of a boundary-column wave's cell (residual_abs<CAVITY> with the
+// indicator products; +-0 terms leave |r| unchanged)
+__device__ __forceinline__ double cav_edge_res(const Coef& c, bool top, double ce, double cw, double pc, double pW,
+                                               double pE, double pS, double pN, double fc) {
+  const double tN = top ? (pN - pc) * 0.0 : (pN - pc);
+  return fabs(c.idx2 * ((pE - pc) * ce + (pW - pc) * cw + tN + (pS - pc)) - fc);
+}
+
 // red (COLOR 0) / black (COLOR 1) update of row j = R - X d (parity JPAR).
 // PROOF (interior waves): the black update also records |p' - p| x wgt
 // (wgt = 1 on rows whose cells prove, 0 elsewhere: a row-uniform scalar).
-template <int DIR, int ROT, int JPAR, int COLOR, bool EDGE, bool PROOF = false>
+// RC (row checks): the row may be a ghost row or the top row; without them
+// (interior bands whose dependency cone stays in rows 1 .. ny-1) every row is
+// updated with four neighbours, straight-line code
+template <int DIR, int ROT, int JPAR, int COLOR, bool EDGE, bool PROOF = false, bool RC = true>
 __device__ __forceinline__ void cav_update(const WaveCtx<CAVITY>& x, double2 (&W)[5], int j, int X,
                                            const double2& fc, double wgt = 0.0, double* dm = nullptr) {
   double2& m = W[CFD_SLOT(X)];
   const double2 bh = W[CFD_SLOT(X + 1)], ah = W[CFD_SLOT(X - 1)];
 #define CFD_S(b, a) ((DIR > 0) ? (b) : (a))
 #define CFD_N(b, a) ((DIR > 0) ? (a) : (b))
-  if (j > x.rmin && j < x.rmax) {  // row-uniform
+  if (!RC || (j > x.rmin && j < x.rmax)) {  // row-uniform
     if (((JPAR ^ COLOR) & 1) == 0) {  // slot a (even column gi) has this colour
       const double Lb = dpp_from_left(m.y);
       if (EDGE) {
-        const double nv = sor_update<CAVITY>(x.c, x.g.nx, x.g.ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x),
-                                             CFD_N(bh.x, ah.x), fc.x);
-        m.x = x.fl_a(j) ? nv : m.x;
+        const double nv = cav_edge_sor(x.c, j == x.g.ny, x.ce_a, x.cw_a, x.om_a, x.om_at, m.x, Lb, m.y,
+                                       CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+        m.x = x.icol_a ? nv : m.x;  // (the rows here are 1..ny)
       } else {
         const double old = m.x;
-        m.x = sor_fast<CAVITY>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+        m.x = RC ? sor_fast<CAVITY>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x)
+                 : sor_interior<CAVITY>(x.c, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
         if (PROOF && COLOR == 1) *dm = fmax(*dm, fabs(m.x - old) * wgt);
       }
     } else {
       const double Ra = dpp_from_right(m.x);
       if (EDGE) {
-        const double nv = sor_update<CAVITY>(x.c, x.g.nx, x.g.ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y),
-                                             CFD_N(bh.y, ah.y), fc.y);
-        m.y = x.fl_b(j) ? nv : m.y;
+        const double nv = cav_edge_sor(x.c, j == x.g.ny, x.ce_b, x.cw_b, x.om_b, x.om_bt, m.y, m.x, Ra,
+                                       CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+        m.y = x.icol_b ? nv : m.y;
       } else {
         const double old = m.y;
-        m.y = sor_fast<CAVITY>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+        m.y = RC ? sor_fast<CAVITY>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y)
+                 : sor_interior<CAVITY>(x.c, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
         if (PROOF && COLOR == 1) *dm = fmax(*dm, fabs(m.y - old) * wgt);
       }
     }
@@ -1260,11 +1320,11 @@ __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const dou
     }
     if (j >= x.g.j0 && j <= x.g.j1) {
       if (EDGE) {
-        const double ra = residual_abs<CAVITY>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
-        const double rb =
-            residual_abs<CAVITY>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
-        rm = fmax(rm, (x.out_lane && x.fl_a(j)) ? ra : 0.0);
-        rm = fmax(rm, (x.out_lane && x.fl_b(j)) ? rb : 0.0);
+        const bool top = j == ny;
+        const double ra = cav_edge_res(c, top, x.ce_a, x.cw_a, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x);
+        const double rb = cav_edge_res(c, top, x.ce_b, x.cw_b, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y);
+        rm = fmax(rm, (x.out_lane && x.icol_a) ? ra : 0.0);  // (rows j0..j1 here)
+        rm = fmax(rm, (x.out_lane && x.icol_b) ? rb : 0.0);
       } else if (j == ny) {  // top row: eps_n = 0 (cavity-01.cpp:666)
         rm = fmax(rm, fmax(residual_abs<CAVITY>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), fc.x),
                            residual_abs<CAVITY>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), fc.y)));
@@ -1280,48 +1340,54 @@ __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const dou
 }
 
 // sweeps S .. NS-1 of one march step (compile-time recursion over the sweeps)
-template <int S, int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF>
+template <int S, int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF, bool RC>
 __device__ __forceinline__ void cav_sweeps(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R) {
   if constexpr (S < NS) {
     // red at R-(2S+1)d (parity PAR^1), black at R-(2S+2)d (PAR), residual at R-(2S+3)d
-    cav_update<DIR, ROT, PAR ^ 1, 0, EDGE>(x, s.w[S], R - (2 * S + 1) * DIR, 2 * S + 1, s.fr[CFD_S10(2 * S + 1)]);
+    cav_update<DIR, ROT, PAR ^ 1, 0, EDGE, false, RC>(x, s.w[S], R - (2 * S + 1) * DIR, 2 * S + 1,
+                                                      s.fr[CFD_S10(2 * S + 1)]);
     if constexpr (PROOF && !EDGE) {
       const int jb = R - (2 * S + 2) * DIR;
       const double wgt = (jb >= x.py0 && jb < x.py1) ? 1.0 : 0.0;  // row-uniform
-      cav_update<DIR, ROT, PAR, 1, EDGE, true>(x, s.w[S], jb, 2 * S + 2, s.fr[CFD_S10(2 * S + 2)], wgt, &s.rmax[S]);
+      cav_update<DIR, ROT, PAR, 1, EDGE, true, RC>(x, s.w[S], jb, 2 * S + 2, s.fr[CFD_S10(2 * S + 2)], wgt,
+                                                   &s.rmax[S]);
     } else {
-      cav_update<DIR, ROT, PAR, 1, EDGE>(x, s.w[S], R - (2 * S + 2) * DIR, 2 * S + 2, s.fr[CFD_S10(2 * S + 2)]);
+      cav_update<DIR, ROT, PAR, 1, EDGE, false, RC>(x, s.w[S], R - (2 * S + 2) * DIR, 2 * S + 2,
+                                                    s.fr[CFD_S10(2 * S + 2)]);
     }
     cav_residual<DIR, ROT, EDGE, PROOF>(x, s.w[S], R - (2 * S + 3) * DIR, 2 * S + 3, s.fr[CFD_S10(2 * S + 3)],
                                         S == NS - 1, PROOF ? s.pm : s.rmax[S]);
     if constexpr (S + 1 < NS) s.w[S + 1][CFD_SLOT(2 * S + 2)] = s.w[S][CFD_SLOT(2 * S + 2)];
-    cav_sweeps<S + 1, NS, DIR, ROT, PAR, EDGE, PROOF>(x, s, R);
+    cav_sweeps<S + 1, NS, DIR, ROT, PAR, EDGE, PROOF, RC>(x, s, R);
   }
 }
 
-template <int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF>  // PAR = parity of R
+template <int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF, int PD, bool RC>  // PAR = parity of R
 __device__ __forceinline__ void cav_step(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R) {
-  s.w[0][CFD_SLOT(0)] = s.np[CFD_SLOT(0)];
-  s.fr[CFD_S10(1)] = s.nf[CFD_SLOT(0)];
+  s.w[0][CFD_SLOT(0)] = s.np[CFD_S10(0)];
+  s.fr[CFD_S10(1)] = s.nf[CFD_S10(1)];
   if (EDGE) {
-    s.np[CFD_SLOT(-4)] = x.ld(x.pin, R + 4 * DIR);
-    s.nf[CFD_SLOT(-4)] = x.ld(x.f, R + 3 * DIR);
+    s.np[CFD_S10(-PD)] = x.ld(x.pin, R + PD * DIR);
+    s.nf[CFD_S10(1 - PD)] = x.ld(x.f, R + (PD - 1) * DIR);
   } else {
-    s.np[CFD_SLOT(-4)] = x.ld_fast(x.pin, R + 4 * DIR);
-    s.nf[CFD_SLOT(-4)] = x.ld_fast(x.f, R + 3 * DIR);
+    s.np[CFD_S10(-PD)] = x.ld_fast(x.pin, R + PD * DIR);
+    s.nf[CFD_S10(1 - PD)] = x.ld_fast(x.f, R + (PD - 1) * DIR);
   }
-  cav_sweeps<0, NS, DIR, ROT, PAR, EDGE, PROOF>(x, s, R);
+  cav_sweeps<0, NS, DIR, ROT, PAR, EDGE, PROOF, RC>(x, s, R);
 }
 
 // PROOF: r[q] = max |black update| of sweep q over the output cells
 // (interior waves; 0 on boundary-column waves), pm = max |p_out| stored
-template <int NS, int DIR, bool EDGE, bool PROOF = false>
-__device__ __forceinline__ void cav_march(const WaveCtx<CAVITY>& x, int y0, int y1, double (&r)[NS],
+template <int NS, int DIR, bool EDGE, bool PROOF = false, bool RC = true,
+          int PD = !PROOF ? CFD_CAV_PD : (NS == 3) ? CFD_CAV_PD3 : CFD_CAV_PD4>
+__device__ __forceinline__ void cav_march(const WaveCtx<CAVITY>& x0, int y0, int y1, double (&r)[NS],
                                           double* pm = nullptr) {
+  WaveCtx<CAVITY> x = x0;
   constexpr int H = 2 * NS + 1;
   const int Rb0 = (DIR > 0) ? y0 - H : y1 - 1 + H;
   const int Rbeg = Rb0 - DIR * (Rb0 & 1);  // even first front row: compile-time colours
   const int nsteps = (y1 - y0) + 2 * H + (Rb0 & 1);
+  if constexpr (EDGE) cav_edge_lanes(x);
   CavRun<NS> s;
   const double2 z = make_double2(0.0, 0.0);
 #pragma unroll
@@ -1334,25 +1400,25 @@ __device__ __forceinline__ void cav_march(const WaveCtx<CAVITY>& x, int y0, int 
   for (int q = 0; q < NS; ++q) s.rmax[q] = 0.0;
   s.pm = 0.0;
   {
-    constexpr int ROT = 0;
+    constexpr int ROT = 0, PAR = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      s.np[CFD_SLOT(-q)] = EDGE ? x.ld(x.pin, Rbeg + q * DIR) : x.ld_fast(x.pin, Rbeg + q * DIR);
-      s.nf[CFD_SLOT(-q)] = EDGE ? x.ld(x.f, Rbeg + (q - 1) * DIR) : x.ld_fast(x.f, Rbeg + (q - 1) * DIR);
+    for (int q = 0; q < PD; ++q) {
+      s.np[CFD_S10(-q)] = EDGE ? x.ld(x.pin, Rbeg + q * DIR) : x.ld_fast(x.pin, Rbeg + q * DIR);
+      s.nf[CFD_S10(1 - q)] = EDGE ? x.ld(x.f, Rbeg + (q - 1) * DIR) : x.ld_fast(x.f, Rbeg + (q - 1) * DIR);
     }
   }
   int R = Rbeg;
   for (int st = 0; st < nsteps; st += 10, R += 10 * DIR) {
-    cav_step<NS, DIR, 0, 0, EDGE, PROOF>(x, s, R);
-    cav_step<NS, DIR, 1, 1, EDGE, PROOF>(x, s, R + DIR);
-    cav_step<NS, DIR, 2, 0, EDGE, PROOF>(x, s, R + 2 * DIR);
-    cav_step<NS, DIR, 3, 1, EDGE, PROOF>(x, s, R + 3 * DIR);
-    cav_step<NS, DIR, 4, 0, EDGE, PROOF>(x, s, R + 4 * DIR);
-    cav_step<NS, DIR, 0, 1, EDGE, PROOF>(x, s, R + 5 * DIR);
-    cav_step<NS, DIR, 1, 0, EDGE, PROOF>(x, s, R + 6 * DIR);
-    cav_step<NS, DIR, 2, 1, EDGE, PROOF>(x, s, R + 7 * DIR);
-    cav_step<NS, DIR, 3, 0, EDGE, PROOF>(x, s, R + 8 * DIR);
-    cav_step<NS, DIR, 4, 1, EDGE, PROOF>(x, s, R + 9 * DIR);
+    cav_step<NS, DIR, 0, 0, EDGE, PROOF, PD, RC>(x, s, R);
+    cav_step<NS, DIR, 1, 1, EDGE, PROOF, PD, RC>(x, s, R + DIR);
+    cav_step<NS, DIR, 2, 0, EDGE, PROOF, PD, RC>(x, s, R + 2 * DIR);
+    cav_step<NS, DIR, 3, 1, EDGE, PROOF, PD, RC>(x, s, R + 3 * DIR);
+    cav_step<NS, DIR, 4, 0, EDGE, PROOF, PD, RC>(x, s, R + 4 * DIR);
+    cav_step<NS, DIR, 0, 1, EDGE, PROOF, PD, RC>(x, s, R + 5 * DIR);
+    cav_step<NS, DIR, 1, 0, EDGE, PROOF, PD, RC>(x, s, R + 6 * DIR);
+    cav_step<NS, DIR, 2, 1, EDGE, PROOF, PD, RC>(x, s, R + 7 * DIR);
+    cav_step<NS, DIR, 3, 0, EDGE, PROOF, PD, RC>(x, s, R + 8 * DIR);
+    cav_step<NS, DIR, 4, 1, EDGE, PROOF, PD, RC>(x, s, R + 9 * DIR);
   }
   if constexpr (PROOF) {
     *pm = s.pm;
@@ -1428,8 +1494,11 @@ struct PairPlan {
 
 // PROOF (cavity): the convergence test of each sweep is the proof above
 // instead of the max-norm residual; the fields are the same bits.
+#ifndef CFD_PROOF_MIN_WAVES
+#define CFD_PROOF_MIN_WAVES 2  // proof-mode launches are planned for 2 waves per SIMD (Solver::init)
+#endif
 template <int CASE, int NS, bool PROOF = false>
-__global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAIR_MIN_WAVES) void poisson_multi_kernel(
+__global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAIR_MIN_WAVES) void poisson_multi_kernel(
     Geo g, Coef c, const double* __restrict__ pin, double* __restrict__ pout, const double* __restrict__ f,
     PoissonCtl ctl, int k, int ka, int kb, PairPlan pl, int flags) {
   // NS red-black iterations k .. k+NS-1 in one launch (NS = 3: cavity only)
@@ -1514,7 +1583,11 @@ __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAI
     if (y1 + 10 <= c.inlet_jmax - 1) cols_in = true;
     else if (y0 - 10 >= c.inlet_jmax + 2 && y1 + 10 <= g.ny && c0 + 128 <= c.step_i - 1) return;
   }
-  const bool up = (flags & 1) && (band & 1);
+  const bool up = CFD_CAV_UP && (flags & 1) && (band & 1);
+  // interior band whose march (rows y0 - 2NS - 2 .. y1 + 2NS + 1: the
+  // dependency cone and the pipeline's own rows) stays inside rows 1 .. ny-1:
+  // no row checks (cav_update RC)
+  const bool safe = y0 - (2 * NS + 2) > x.rmin && y1 + (2 * NS + 2) < min(x.rmax, g.ny);
   // flags bit 4 / bit 5 (timing diagnostics only): never / always take the interior path
   // (the proof needs four-neighbour cells: never forced onto the interior path)
   const bool fast = PROOF ? cols_in : ((flags & 32) || (!(flags & 16) && cols_in));
@@ -1525,6 +1598,8 @@ __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAI
       x.py1 = min(y1, g.ny);
       double pm = 0.0;
       if (!fast) cav_march<NS, 1, true, true>(x, y0, y1, r, &pm);
+      else if (safe && up) cav_march<NS, -1, false, true, false>(x, y0, y1, r, &pm);
+      else if (safe) cav_march<NS, 1, false, true, false>(x, y0, y1, r, &pm);
       else if (up) cav_march<NS, -1, false, true>(x, y0, y1, r, &pm);
       else cav_march<NS, 1, false, true>(x, y0, y1, r, &pm);
       // P bound of this launch: max|p_out| of the launch before (ring slot of
@@ -1547,6 +1622,8 @@ __global__ __launch_bounds__(256, (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAI
                   (unsigned long long)__double_as_longlong(pm));
     } else {
       if (!fast) cav_march<NS, 1, true>(x, y0, y1, r);
+      else if (safe && up) cav_march<NS, -1, false, false, false>(x, y0, y1, r);
+      else if (safe) cav_march<NS, 1, false, false, false>(x, y0, y1, r);
       else if (up) cav_march<NS, -1, false>(x, y0, y1, r);
       else cav_march<NS, 1, false>(x, y0, y1, r);
     }

@@ -140,7 +140,7 @@ class Solver {
   bool proof_launch = false;  // the launch being enqueued runs in proof mode
   bool window_proof = false;  // the window it tests was computed in proof mode
   bool proof_enabled = true;  // CFD_PROOF=0: exact residuals throughout
-  int proof_ns = 3;           // sweeps per proof-mode launch (3 or 4: CFD_PROOF_NS)
+  int proof_ns = 4;           // sweeps per proof-mode launch (4; 3: CFD_PROOF_NS=3)
   bool proof_ok() const {
     // (only interior column tiles prove: at least one between the two boundary tiles)
     return proof_enabled && P.case_id == CFD_CAVITY && sweeps_per_launch() == 3 && C.proof_k > 0.0 &&
@@ -161,7 +161,7 @@ class Solver {
   cfd_timing T{};
   int resident_waves = 2048;  // wave-march tiles in flight (CUs x 4 SIMDs x waves per SIMD)
   int resident_pair_waves = 2048;  // the same for the two-iteration kernel
-  int pair_edge_pct = 45;          // boundary-column band length, % of the interior march (swept, cavity triples: 40-47 best)
+  int pair_edge_pct = 45;          // boundary-column band length, % of the interior march (open cases; cavity: 80)
   int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order
   int march_min_th = MARCH_MIN_TH;
 
@@ -201,6 +201,8 @@ class Solver {
     }
     validate();
     C = make_coef(P);
+    if (const char* e = std::getenv("CFD_PROOF")) proof_enabled = std::atoi(e) != 0;  // 0: exact residuals throughout
+    if (const char* e = std::getenv("CFD_PROOF_NS")) proof_ns = std::atoi(e) == 3 ? 3 : 4;
     HIPC(hipSetDevice(dev));
     hipDeviceProp_t prop;
     HIPC(hipGetDeviceProperties(&prop, dev));
@@ -221,6 +223,15 @@ class Solver {
       else
         HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pps, poisson_multi_kernel<BACKSTEP, 2>, 256, 0));
       pps = std::max(1, std::min(pps, 4));
+      if (P.case_id == CFD_CAVITY) {
+        // cavity launches (boundary-column waves with lane-constant indicators,
+        // nearly as fast as interior ones): boundary bands 80 % of the interior
+        // march; proof-mode launches planned for 2 waves per SIMD (taller
+        // bands: fewer halo rows), exact ones for 3 (measured at 4096^2,
+        // DESIGN.md §4)
+        pair_edge_pct = 80;
+        if (proof_ok()) pps = std::min(pps, 2);
+      }
       if (const char* e = std::getenv("CFD_PAIR_WPS")) pps = std::max(1, std::atoi(e));
       if (use_lexw()) {
         int lps = 0;
@@ -235,8 +246,6 @@ class Solver {
       if (const char* e = std::getenv("CFD_MARCH_MIN_TH")) march_min_th = std::max(1, std::atoi(e));  // tuning
       resident_pair_waves = pps * 4 * prop.multiProcessorCount;
     }
-    if (const char* e = std::getenv("CFD_PROOF")) proof_enabled = std::atoi(e) != 0;  // 0: exact residuals throughout
-    if (const char* e = std::getenv("CFD_PROOF_NS")) proof_ns = std::atoi(e) == 4 ? 4 : 3;
     pitch = ((P.nx + 3) + 15) / 16 * 16;  // >= nx+3: column pairs (gi, gi+1) stay inside a row
     size_t part = 0;
     for (auto [j0, j1] : rows) {
