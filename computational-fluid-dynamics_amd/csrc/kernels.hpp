@@ -1173,7 +1173,7 @@ struct CavRun {
   double2 np[10];    // prefetched p_in rows R .. R+PD d (row R - X d in slot CFD_S10(X))
   double2 nf[10];    // prefetched f rows R-d .. R+(PD-1) d (same slots)
   double rmax[NS];   // exact mode: max |residual| per sweep; proof mode: max |black update| per sweep
-  double pm;         // proof mode: max |p_out| over the cells this wave stores
+  double pm;         // proof mode: max |p_in| over every row this wave loads (all lanes)
 };
 
 // ---------------------------------------------- proof-mode convergence test --
@@ -1189,8 +1189,9 @@ struct CavRun {
 // bound on every |p| in the cell's stencil, F on |f|; DESIGN.md §2 has the
 // derivation; requires 0.5 <= w < 2). Each sweep grows max|p| by at most 9x
 // (red then black, w < 2) plus h^2 F, so over a launch P <= 9^NS (Pin + h^2 F),
-// Pin = max|p_in| (every launch records max|p_out|; the solve starts from
-// zero) and F = max|f| over the interior (tolerance pass). Hence
+// Pin = max|p_in| over every value the wave loads (all its cells' cones lie in
+// them: no cross-wave or cross-rank bound needed) and F = max|f| over the
+// interior (tolerance pass). Hence
 //     |p' - p| > thr = (tol + 2^-43 (idx2 P + F)) / |K|  (x (1 + 2^-38))
 // proves |r_ref| > tol, i.e. the reference's loop goes on, with the computed
 // fields untouched. The wave records max|p' - p| / thr per sweep (> 1:
@@ -1294,10 +1295,10 @@ __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const dou
   const Coef& c = x.c;
 #define CFD_S(b, a) ((DIR > 0) ? (b) : (a))
 #define CFD_N(b, a) ((DIR > 0) ? (a) : (b))
-  if (PROOF) {  // no residual: the store of the last sweep, and max|p_out| (in rm)
+  if (PROOF) {  // no residual: the store of the last sweep
+    (void)rm;
     if (store && j >= x.y0 && j < x.y1 && x.out_lane) {
       const double2 m = W[CFD_SLOT(X)];
-      rm = fmax(rm, fmax(fabs(m.x), fabs(m.y)));
       double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
       typedef double d2v __attribute__((ext_vector_type(2)));
       d2v mv = {m.x, m.y};
@@ -1356,7 +1357,7 @@ __device__ __forceinline__ void cav_sweeps(const WaveCtx<CAVITY>& x, CavRun<NS>&
                                                     s.fr[CFD_S10(2 * S + 2)]);
     }
     cav_residual<DIR, ROT, EDGE, PROOF>(x, s.w[S], R - (2 * S + 3) * DIR, 2 * S + 3, s.fr[CFD_S10(2 * S + 3)],
-                                        S == NS - 1, PROOF ? s.pm : s.rmax[S]);
+                                        S == NS - 1, s.rmax[S]);
     if constexpr (S + 1 < NS) s.w[S + 1][CFD_SLOT(2 * S + 2)] = s.w[S][CFD_SLOT(2 * S + 2)];
     cav_sweeps<S + 1, NS, DIR, ROT, PAR, EDGE, PROOF, RC>(x, s, R);
   }
@@ -1366,6 +1367,10 @@ template <int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF, int PD, bool
 __device__ __forceinline__ void cav_step(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R) {
   s.w[0][CFD_SLOT(0)] = s.np[CFD_S10(0)];
   s.fr[CFD_S10(1)] = s.nf[CFD_S10(1)];
+  if constexpr (PROOF && !EDGE) {  // the proof's Pin: every p_in value this wave uses
+    const double2 a = s.np[CFD_S10(0)];
+    s.pm = fmax(s.pm, fmax(fabs(a.x), fabs(a.y)));
+  }
   if (EDGE) {
     s.np[CFD_S10(-PD)] = x.ld(x.pin, R + PD * DIR);
     s.nf[CFD_S10(1 - PD)] = x.ld(x.f, R + (PD - 1) * DIR);
@@ -1377,7 +1382,7 @@ __device__ __forceinline__ void cav_step(const WaveCtx<CAVITY>& x, CavRun<NS>& s
 }
 
 // PROOF: r[q] = max |black update| of sweep q over the output cells
-// (interior waves; 0 on boundary-column waves), pm = max |p_out| stored
+// (interior waves; 0 on boundary-column waves), pm = max |p_in| loaded
 template <int NS, int DIR, bool EDGE, bool PROOF = false, bool RC = true,
           int PD = !PROOF ? CFD_CAV_PD : (NS == 3) ? CFD_CAV_PD3 : CFD_CAV_PD4>
 __device__ __forceinline__ void cav_march(const WaveCtx<CAVITY>& x0, int y0, int y1, double (&r)[NS],
@@ -1520,7 +1525,6 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
 #pragma unroll
     for (int q = 0; q < NS; ++q)
       ctl.ring[(size_t)((k + NS + q) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
-    if (PROOF && lane == 0) ctl.ring[(size_t)((k + NS) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + 1] = 0.0;
   }
 
   const int nblk = (int)gridDim.x;
@@ -1602,24 +1606,12 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
       else if (safe) cav_march<NS, 1, false, true, false>(x, y0, y1, r, &pm);
       else if (up) cav_march<NS, -1, false, true>(x, y0, y1, r, &pm);
       else cav_march<NS, 1, false, true>(x, y0, y1, r, &pm);
-      // P bound of this launch: max|p_out| of the launch before (ring slot of
-      // its first iteration, element 1), or with the lagged test (ranks; that
-      // one's maximum may not be all-reduced yet) of the launch before that,
-      // grown over one more launch; none before the first launch (the solve
-      // starts from a zero field)
-      const bool lag = (flags & 256) != 0;
-      const int kp = k - (lag ? 2 * NS : NS);
-      double pin = (kp >= 1) ? ctl.ring[(size_t)(kp & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + 1] : 0.0;
+      // P bound: this wave's own max|p_in| (its cells' cones lie in what it
+      // loaded), grown over the launch's sweeps
       constexpr double growth = (NS == 2) ? 81.0 : (NS == 3) ? 729.0 : 6561.0;
-      const double F = ctl.tol[2];
-      if (lag) pin = growth * (pin + c.h2 * F) * (1.0 + 0x1p-40);
-      const double tol = ctl.tol[0];
-      pm = wave_max(pm);
+      const double pin = wave_max(pm), F = ctl.tol[2], tol = ctl.tol[0];
 #pragma unroll
       for (int q = 0; q < NS; ++q) r[q] = proof_ratio(c, tol, wave_max(r[q]), pin, F, growth);
-      if (lane == 0 && pm > 0.0)  // this launch's max|p_out| (zeroed by the launch before)
-        atomicMax(reinterpret_cast<unsigned long long*>(ctl.ring + (size_t)(k & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + 1),
-                  (unsigned long long)__double_as_longlong(pm));
     } else {
       if (!fast) cav_march<NS, 1, true>(x, y0, y1, r);
       else if (safe && up) cav_march<NS, -1, false, false, false>(x, y0, y1, r);

@@ -151,7 +151,7 @@ class Solver {
 
   // enqueue the pending (lagged) all-reduce of an overlapped launch on xs
   void flush_allreduce(hipStream_t xs) {
-    if (ar_pending.n > 0) allreduce_slots(ar_pending.first, ar_pending.n, xs, ar_pending.proof);
+    if (ar_pending.n > 0) allreduce_slots(ar_pending.first, ar_pending.n, xs);
     ar_pending = {0, 0};
   }
   int nbufs() const { return lagged() ? 3 : 2; }
@@ -597,8 +597,7 @@ class Solver {
                     const PoissonCtl& ctl, int k, int ka, int kb, hipStream_t stream, bool replay = false) {
     // bit 2: no test at all (the solve has already stopped); bit 7: the tested
     // window holds proof ratios (it was computed by a proof-mode launch)
-    // bit 8: proof-mode P bound from the launch before the previous one (lagged test)
-    const int fl = march_flags | (replay ? 4 : 0) | (window_proof ? 128 : 0) | (lagged() ? 256 : 0);
+    const int fl = march_flags | (replay ? 4 : 0) | (window_proof ? 128 : 0);
     const int ne = pl.ctiles >= 2 ? 2 : 1;
     const int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
     if (ntiles == 0) return;
@@ -651,8 +650,7 @@ class Solver {
 
   // all-reduce (max) of the residual slots of iterations k .. k+n-1 that are tested
   // (slots adjacent in the ring go in one call: one RCCL latency per launch)
-  // (a proof-mode launch: its first slot also holds its max|p_out|, always reduced)
-  void allreduce_slots(int k, int n, hipStream_t xs, bool proof) {
+  void allreduce_slots(int k, int n, hipStream_t xs) {
     constexpr size_t SLOT = (size_t)RES_SHARDS * SHARD_STRIDE;
     int run0 = -1, runn = 0;  // ring slots [run0, run0 + runn) pending
     auto flush = [&] {
@@ -660,7 +658,7 @@ class Solver {
       runn = 0;
     };
     for (int kk = k; kk < k + n && kk <= P.max_iters; ++kk) {
-      if (!(kk % P.check_every == 0 || kk == P.max_iters || (proof && kk == k))) continue;
+      if (!(kk % P.check_every == 0 || kk == P.max_iters)) continue;
       const int sl = kk & (RING - 1);
       if (runn > 0 && sl == run0 + runn) {
         ++runn;
@@ -744,7 +742,7 @@ class Solver {
     if (P.case_id == CFD_CAVITY) launch_poisson<CAVITY>(pin.data(), pout.data(), k, n, ka, kb, replay);
     else if (P.case_id == CFD_CHANNEL) launch_poisson<CHANNEL>(pin.data(), pout.data(), k, n, ka, kb, replay);
     else launch_poisson<BACKSTEP>(pin.data(), pout.data(), k, n, ka, kb, replay);
-    if (comm && comm->nranks > 1 && !replay) allreduce_slots(k, n, st, proof_launch);
+    if (comm && comm->nranks > 1 && !replay) allreduce_slots(k, n, st);
   }
 
   // solverPressurePoisson (cavity-01.cpp:609-690, channel-01.cpp:635-688,

@@ -35,7 +35,8 @@ def run_ranks(cp, world, steps, check_every=1, timing=False):
             its = [s.step() for _ in range(steps)]
             md, ke = s.statistics()
             results[r] = dict(rows=s.owned_rows(), u=s.field("u"), v=s.field("v"), p=s.field("p"), its=its,
-                              stats=(md, ke), overlapped=s.timing().poisson_overlapped)
+                              stats=(md, ke), overlapped=s.timing().poisson_overlapped,
+                              fallbacks=s.timing().proof_fallbacks)
             s.close()
             L.cfd_comm_destroy(comm)
         except Exception as e:  # noqa: BLE001
@@ -146,6 +147,33 @@ def test_overlapped_lagged_stop_and_caps(delta):
     for r in res:
         assert r["overlapped"] > 0
         assert r["its"] == its, (K, delta)
+        j0, j1 = r["rows"]
+        first = 0 if j0 == 1 else j0
+        last = min(j1 + 1 if j1 == cp.ny else j1, ref.shape[0] - 1)
+        assert np.array_equal(r["p"].view(np.int64), ref[first:last + 1].view(np.int64))
+
+
+@pytest.mark.parametrize("world,nx,ny,steps,cap", [(2, 256, 256, 3, 0), (3, 300, 240, 2, 0), (2, 512, 512, 2, 61)])
+def test_proof_mode_on_ranks(monkeypatch, world, nx, ny, steps, cap):
+    """The proof-mode convergence test on ranks: interior column
+    tiles (nx >= 240), overlapped strips with the lagged test, ratios
+    all-reduced (max) like residuals. Iteration counts and fields must equal
+    one domain with exact residuals, bit for bit."""
+    kw = {"max_iters": cap} if cap else {}
+    cp = C.make_params("cavity", nx=nx, ny=ny, **kw)
+    monkeypatch.setenv("CFD_SMALL", "0")
+    monkeypatch.setenv("CFD_PROOF", "0")
+    s, its = single(cp, steps)
+    ref = s.field("p")
+    monkeypatch.setenv("CFD_PROOF", "1")
+    res = run_ranks(cp, world, steps)
+    for r in res:
+        assert r["overlapped"] > 0
+        assert r["its"] == its
+        if cap:
+            assert r["fallbacks"] == 1  # the first step's corner-only source (tests/test_gpu_proof.py)
+        else:
+            assert r["fallbacks"] >= sum(1 for k, _ in its if k < cp.max_iters)
         j0, j1 = r["rows"]
         first = 0 if j0 == 1 else j0
         last = min(j1 + 1 if j1 == cp.ny else j1, ref.shape[0] - 1)
