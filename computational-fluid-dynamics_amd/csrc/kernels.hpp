@@ -237,6 +237,12 @@ __global__ void bc_step_faces_kernel(Geo g, Coef c, double* __restrict__ u, doub
 // wave's columns 1..126 (TENT_TWC per tile). Same expressions in the same
 // order as the reference loops, hence the same bits.
 constexpr int TENT_TWC = 126;
+#ifndef CFD_TENT_PD
+#define CFD_TENT_PD 3  // rows of u and v in flight ahead of row j+1
+#endif
+#ifndef CFD_TENT_NT
+#define CFD_TENT_NT 0  // nontemporal u*, v* stores
+#endif
 __global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const double* __restrict__ u,
                                                         const double* __restrict__ v, double* __restrict__ us,
                                                         double* __restrict__ vs, int th, int ctiles) {
@@ -259,14 +265,23 @@ __global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const dou
   // rows past y1 are never consumed)
   const int rlast = g.row_lo + g.nrows - 1;
   auto ldc = [&](const double* base, int j) { return ld(base, min(j, rlast)); };
+  constexpr int PD = CFD_TENT_PD;
   double2 um = ld(u, y0 - 1), uc = ld(u, y0), vm = ld(v, y0 - 1), vc = ld(v, y0);
-  double2 uq0 = ldc(u, y0 + 1), vq0 = ldc(v, y0 + 1), uq1 = ldc(u, y0 + 2), vq1 = ldc(v, y0 + 2);
-  double2 uq2 = ldc(u, y0 + 3), vq2 = ldc(v, y0 + 3);
+  double2 uq[PD], vq[PD];
+#pragma unroll
+  for (int q = 0; q < PD; ++q) {
+    uq[q] = ldc(u, y0 + 1 + q);
+    vq[q] = ldc(v, y0 + 1 + q);
+  }
   for (int j = y0; j < y1; ++j) {
-    const double2 up = uq0, vp = vq0;
-    uq0 = uq1; vq0 = vq1; uq1 = uq2; vq1 = vq2;
-    uq2 = ldc(u, j + 4);
-    vq2 = ldc(v, j + 4);
+    const double2 up = uq[0], vp = vq[0];
+#pragma unroll
+    for (int q = 0; q + 1 < PD; ++q) {
+      uq[q] = uq[q + 1];
+      vq[q] = vq[q + 1];
+    }
+    uq[PD - 1] = ldc(u, j + 1 + PD);
+    vq[PD - 1] = ldc(v, j + 1 + PD);
     const double uWa = dpp_from_left(uc.y), uEb = dpp_from_right(uc.x);
     const double vEb = dpp_from_right(vc.x), vmEb = dpp_from_right(vm.x);
     const double vWa = dpp_from_left(vc.y), upWa = dpp_from_left(up.y);
@@ -320,14 +335,16 @@ __global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const dou
     typedef double d2v __attribute__((ext_vector_type(2)));
     if (ua && ub) {
       d2v w = {usv[0], usv[1]};
-      *reinterpret_cast<d2v*>(usr + gi) = w;
+      if (CFD_TENT_NT) __builtin_nontemporal_store(w, reinterpret_cast<d2v*>(usr + gi));
+      else *reinterpret_cast<d2v*>(usr + gi) = w;
     } else {
       if (ua) usr[gi] = usv[0];
       if (ub) usr[gi + 1] = usv[1];
     }
     if (va && vb) {
       d2v w = {vsv[0], vsv[1]};
-      *reinterpret_cast<d2v*>(vsr + gi) = w;
+      if (CFD_TENT_NT) __builtin_nontemporal_store(w, reinterpret_cast<d2v*>(vsr + gi));
+      else *reinterpret_cast<d2v*>(vsr + gi) = w;
     } else {
       if (va) vsr[gi] = vsv[0];
       if (vb) vsr[gi + 1] = vsv[1];
@@ -941,7 +958,9 @@ __device__ __forceinline__ double sor_fast(const WaveCtx<CASE>& x, int j, double
 // dependency cone are interior fluid cells of rows that are updated (checked
 // per wave by the caller), so no per-cell masks are evaluated; the residual
 // of halo lanes is masked once at the end instead of per row.
-template <int CASE, int DIR, int ROT, int OFF, bool FAST, int APAR>
+// RC (FAST only): row checks; without them (bands whose march stays off the
+// ghost rows) every row is updated and nothing is refreshed, straight-line
+template <int CASE, int DIR, int ROT, int OFF, bool FAST, int APAR, bool RC = true>
 __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)[5], double2 (&Q)[5],
                                             const double2& f_red, const double2& f_black, const double2& f_res,
                                             int A, bool store, double& rm) {
@@ -956,7 +975,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     if ((APAR == 2) ? ((j & 1) == 0) : ((APAR ^ 1) == 0)) {  // APAR 2: parity known at run time only
       const double Lb = dpp_from_left(m.y);
       if (FAST) {
-        if (j > x.rmin && j < x.rmax) m.x = sor_fast<CASE>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
+        if (!RC || (j > x.rmin && j < x.rmax)) m.x = sor_fast<CASE>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
@@ -965,7 +984,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     } else {
       const double Ra = dpp_from_right(m.x);
       if (FAST) {
-        if (j > x.rmin && j < x.rmax) m.y = sor_fast<CASE>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
+        if (!RC || (j > x.rmin && j < x.rmax)) m.y = sor_fast<CASE>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
@@ -980,7 +999,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     if ((APAR == 2) ? ((j & 1) == 1) : (APAR == 1)) {
       const double Lb = dpp_from_left(m.y);
       if (FAST) {
-        if (j > x.rmin && j < x.rmax) m.x = sor_fast<CASE>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
+        if (!RC || (j > x.rmin && j < x.rmax)) m.x = sor_fast<CASE>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
@@ -989,7 +1008,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     } else {
       const double Ra = dpp_from_right(m.x);
       if (FAST) {
-        if (j > x.rmin && j < x.rmax) m.y = sor_fast<CASE>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
+        if (!RC || (j > x.rmin && j < x.rmax)) m.y = sor_fast<CASE>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
@@ -1000,7 +1019,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
   {  // ghost / solid refresh at row A-3d (pre-refresh neighbours) -> Q; none for interior fluid cells
     const double2 m = W[CFD_SLOT(3 + OFF)];
     double2 nv = m;
-    if (CASE != CAVITY && FAST) {  // interior columns: only the ghost rows refresh (row-uniform)
+    if (CASE != CAVITY && FAST && RC) {  // interior columns: only the ghost rows refresh (row-uniform)
       const int j = A - 3 * DIR;
       // values picked at compile time: a ?: between the two ring elements
       // became a select of addresses, which put the whole ring in scratch
@@ -1043,7 +1062,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
 #endif
       }
       if (FAST) {
-        if (j >= x.g.j0 && j <= x.g.j1) {  // row-uniform
+        if (!RC || (j >= x.g.j0 && j <= x.g.j1)) {  // row-uniform
           if (CASE == CAVITY && j == ny) {  // top row: eps_n = 0 (cavity-01.cpp:666)
             rm = fmax(rm, residual_abs<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x));
             rm = fmax(rm, residual_abs<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_res.y));
@@ -1072,7 +1091,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
 // 10 from ROT = t mod 5 and PAR = t mod 2; NPR == 5 only needs ROT)
 #define CFD_NSLOT(X) ((NPR == 5) ? CFD_SLOT(X) : ((((6 * (ROT) + 5 * (PAR)) % 10 + NPR - 1 - (X)) % NPR + 2 * NPR) % NPR))
 
-template <int CASE, int DIR, int ROT, bool FAST, int PAR, int NPR>  // PAR = parity of R (2: not known at compile time)
+template <int CASE, int DIR, int ROT, bool FAST, int PAR, int NPR, bool RC = true>  // PAR = parity of R (2: not known at compile time)
 __device__ __forceinline__ void wave_pair_step(const WaveCtx<CASE>& x, WavePair<NPR>& s, int R) {
   constexpr int PD = NPR - 1;  // rows in flight ahead of the front row
   static_assert(NPR == 5 || PAR != 2, "deep prefetch rings need the 10-step unroll");
@@ -1088,15 +1107,15 @@ __device__ __forceinline__ void wave_pair_step(const WaveCtx<CASE>& x, WavePair<
     s.nf[CFD_NSLOT(-PD)] = x.ld(x.f, R + (PD - 1) * DIR);
   }
   // iteration k: rows R-d .. R-4d
-  pair_stages<CASE, DIR, ROT, 0, FAST, PAR>(x, s.w, s.q, s.fr[CFD_SLOT(1)], s.fr[CFD_SLOT(2)], s.fr[CFD_SLOT(4)], R, false,
+  pair_stages<CASE, DIR, ROT, 0, FAST, PAR, RC>(x, s.w, s.q, s.fr[CFD_SLOT(1)], s.fr[CFD_SLOT(2)], s.fr[CFD_SLOT(4)], R, false,
                                        s.rmax1);
   // iteration k+1 takes iteration k's newest final row (R-3d) as its front row
   s.w2[CFD_SLOT(3)] = s.q[CFD_SLOT(3)];
-  pair_stages<CASE, DIR, ROT, 3, FAST, (PAR == 2) ? 2 : (PAR ^ 1)>(x, s.w2, s.q2, s.fr[CFD_SLOT(4)], s.fr[CFD_SLOT(5)], s.fr2[CFD_SLOT(7)],
+  pair_stages<CASE, DIR, ROT, 3, FAST, (PAR == 2) ? 2 : (PAR ^ 1), RC>(x, s.w2, s.q2, s.fr[CFD_SLOT(4)], s.fr[CFD_SLOT(5)], s.fr2[CFD_SLOT(7)],
                                        R - 3 * DIR, true, s.rmax2);
 }
 
-template <int CASE, int DIR, bool FAST>
+template <int CASE, int DIR, bool FAST, bool RC = true>
 __device__ __forceinline__ void wave_march_pair(const WaveCtx<CASE>& x, int y0, int y1, double& r1, double& r2) {
   constexpr int H = PAIR_H;
   // first front row, moved one row outward if needed so that it is even: the
@@ -1123,16 +1142,16 @@ __device__ __forceinline__ void wave_march_pair(const WaveCtx<CASE>& x, int y0, 
   }
   int R = Rbeg;
   for (int st = 0; st < nsteps; st += 10, R += 10 * DIR) {
-    wave_pair_step<CASE, DIR, 0, FAST, 0, NPR>(x, s, R);
-    wave_pair_step<CASE, DIR, 1, FAST, 1, NPR>(x, s, R + DIR);
-    wave_pair_step<CASE, DIR, 2, FAST, 0, NPR>(x, s, R + 2 * DIR);
-    wave_pair_step<CASE, DIR, 3, FAST, 1, NPR>(x, s, R + 3 * DIR);
-    wave_pair_step<CASE, DIR, 4, FAST, 0, NPR>(x, s, R + 4 * DIR);
-    wave_pair_step<CASE, DIR, 0, FAST, 1, NPR>(x, s, R + 5 * DIR);
-    wave_pair_step<CASE, DIR, 1, FAST, 0, NPR>(x, s, R + 6 * DIR);
-    wave_pair_step<CASE, DIR, 2, FAST, 1, NPR>(x, s, R + 7 * DIR);
-    wave_pair_step<CASE, DIR, 3, FAST, 0, NPR>(x, s, R + 8 * DIR);
-    wave_pair_step<CASE, DIR, 4, FAST, 1, NPR>(x, s, R + 9 * DIR);
+    wave_pair_step<CASE, DIR, 0, FAST, 0, NPR, RC>(x, s, R);
+    wave_pair_step<CASE, DIR, 1, FAST, 1, NPR, RC>(x, s, R + DIR);
+    wave_pair_step<CASE, DIR, 2, FAST, 0, NPR, RC>(x, s, R + 2 * DIR);
+    wave_pair_step<CASE, DIR, 3, FAST, 1, NPR, RC>(x, s, R + 3 * DIR);
+    wave_pair_step<CASE, DIR, 4, FAST, 0, NPR, RC>(x, s, R + 4 * DIR);
+    wave_pair_step<CASE, DIR, 0, FAST, 1, NPR, RC>(x, s, R + 5 * DIR);
+    wave_pair_step<CASE, DIR, 1, FAST, 0, NPR, RC>(x, s, R + 6 * DIR);
+    wave_pair_step<CASE, DIR, 2, FAST, 1, NPR, RC>(x, s, R + 7 * DIR);
+    wave_pair_step<CASE, DIR, 3, FAST, 0, NPR, RC>(x, s, R + 8 * DIR);
+    wave_pair_step<CASE, DIR, 4, FAST, 1, NPR, RC>(x, s, R + 9 * DIR);
   }
   r1 = FAST ? (x.out_lane ? s.rmax1 : 0.0) : s.rmax1;
   r2 = FAST ? (x.out_lane ? s.rmax2 : 0.0) : s.rmax2;
@@ -1622,7 +1641,12 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
   } else {
     double r1 = 0.0, r2 = 0.0;
     if (fast) {
-      if (up) wave_march_pair<CASE, -1, true>(x, y0, y1, r1, r2);
+      // bands whose march (rows y0 - 9 .. y1 + 8) stays off the ghost rows:
+      // no row checks, no refresh
+      const bool osafe = y0 - (PAIR_H + 2) > x.rmin && y1 + (PAIR_H + 2) < min(x.rmax, g.ny + 1);
+      if (osafe && up) wave_march_pair<CASE, -1, true, false>(x, y0, y1, r1, r2);
+      else if (osafe) wave_march_pair<CASE, 1, true, false>(x, y0, y1, r1, r2);
+      else if (up) wave_march_pair<CASE, -1, true>(x, y0, y1, r1, r2);
       else wave_march_pair<CASE, 1, true>(x, y0, y1, r1, r2);
     } else {  // boundary-column waves march one way (compact code)
       wave_march_pair_edge<CASE, 1>(x, y0, y1, r1, r2);
