@@ -1042,12 +1042,18 @@ class Solver {
     double* d_res = total + 2;
     HIPC(hipEventRecord(ev_a, st));
     const int ce = std::max(1, P.check_every);
-    const bool fl = 2LL * (P.nx + 2) * (P.ny + 2) <= SMALL_CELLS;  // f in LDS too
-#define CFD_SMALL_LAUNCH(CASE)                                                                                  \
-  if (fl) poisson_small_kernel<CASE, true><<<1, SMALL_THREADS, 0, st>>>(s.g, C, X, s.b[B_F], tolv, P.max_iters, ce, \
-                                                                        d_it, d_res);                          \
-  else poisson_small_kernel<CASE, false><<<1, SMALL_THREADS, 0, st>>>(s.g, C, X, s.b[B_F], tolv, P.max_iters, ce,  \
-                                                                       d_it, d_res)
+    const long long per_colour = ((long long)P.nx * P.ny + 1) / 2;
+    const int maxc = per_colour <= 2 * SMALL_THREADS ? 2 : per_colour <= 4 * SMALL_THREADS ? 4
+                   : per_colour <= 8 * SMALL_THREADS ? 8 : SMALL_MAXC;
+#define CFD_SMALL_LAUNCH(CASE)                                                                                    \
+  if (maxc == 2)                                                                                                  \
+    poisson_small_kernel<CASE, 2><<<1, SMALL_THREADS, 0, st>>>(s.g, C, X, s.b[B_F], tolv, P.max_iters, ce, d_it, d_res); \
+  else if (maxc == 4)                                                                                             \
+    poisson_small_kernel<CASE, 4><<<1, SMALL_THREADS, 0, st>>>(s.g, C, X, s.b[B_F], tolv, P.max_iters, ce, d_it, d_res); \
+  else if (maxc == 8)                                                                                             \
+    poisson_small_kernel<CASE, 8><<<1, SMALL_THREADS, 0, st>>>(s.g, C, X, s.b[B_F], tolv, P.max_iters, ce, d_it, d_res); \
+  else                                                                                                            \
+    poisson_small_kernel<CASE, SMALL_MAXC><<<1, SMALL_THREADS, 0, st>>>(s.g, C, X, s.b[B_F], tolv, P.max_iters, ce, d_it, d_res)
     if (P.case_id == CFD_CAVITY) { CFD_SMALL_LAUNCH(CAVITY); }
     else if (P.case_id == CFD_CHANNEL) { CFD_SMALL_LAUNCH(CHANNEL); }
     else { CFD_SMALL_LAUNCH(BACKSTEP); }
