@@ -75,7 +75,13 @@ def cpu_baseline(nx: int, ny: int, budget_s: float, case: str = "cavity") -> dic
             break
     del o
     mlups = nx * ny * n / el / 1e6
-    return {"value": round(mlups, 3), "unit": "MLUPS", "cores": 1, "kind": "port",
+    cpu_model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), None)
+    except OSError:
+        pass
+    return {"value": round(mlups, 3), "unit": "MLUPS", "cores": 1, "kind": "port", "cpu_model": cpu_model,
             "sample": f"{n} lexicographic SOR sweeps + residual (reference loop restated in C, gcc -O2) on the "
                       f"{nx}x{ny} {case} after one predictor step, {el:.1f} s single-threaded"}
 

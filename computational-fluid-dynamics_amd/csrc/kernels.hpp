@@ -236,7 +236,10 @@ __global__ void bc_step_faces_kernel(Geo g, Coef c, double* __restrict__ u, doub
 // 2 halo rows per band and 2 halo columns per 128). Output columns: the
 // wave's columns 1..126 (TENT_TWC per tile). Same expressions in the same
 // order as the reference loops, hence the same bits.
-constexpr int TENT_TWC = 126;
+#ifndef CFD_TENT_ALIGN
+#define CFD_TENT_ALIGN 0  // 1: tiles of 112 output columns starting on 128-B lines (lanes 4..59 store)
+#endif
+constexpr int TENT_TWC = CFD_TENT_ALIGN ? 112 : 126;
 #ifndef CFD_TENT_PD
 #define CFD_TENT_PD 3  // rows of u and v in flight ahead of row j+1
 #endif
@@ -253,14 +256,16 @@ __global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const dou
   if (y0 >= y1) return;
   const int nx = g.nx, ny = g.ny;
   const bool step = c.case_id == BACKSTEP;
-  const int gi = ctile * TENT_TWC + 2 * lane;      // this lane's columns gi (a), gi + 1 (b)
-  const int gic = min(gi, g.pitch - 2);             // (lanes past the row read a valid pair)
+  // this lane's columns gi (a), gi + 1 (b)
+  const int gi = CFD_TENT_ALIGN ? ctile * TENT_TWC - 8 + 2 * lane : ctile * TENT_TWC + 2 * lane;
+  const int gic = max(min(gi, g.pitch - 2), 0);     // (lanes past the row read a valid pair)
   const size_t P = (size_t)g.pitch;
   auto ld = [&](const double* base, int j) {
     return *reinterpret_cast<const double2*>(base + (size_t)(j - g.row_lo) * P + gic);
   };
   // output cells: a of lanes 1..63, b of lanes 0..62 (their row neighbours are in the wave)
-  const bool out_a = lane >= 1 && gi <= nx, out_b = lane <= 62 && gi + 1 <= nx;
+  const bool out_a = (CFD_TENT_ALIGN ? lane >= 4 && lane <= 59 : lane >= 1) && gi <= nx;
+  const bool out_b = (CFD_TENT_ALIGN ? lane >= 4 && lane <= 59 : lane <= 62) && gi + 1 <= nx;
   // rows j+1 .. j+3 of u and v in flight (clamped to the strip's stored rows:
   // rows past y1 are never consumed)
   const int rlast = g.row_lo + g.nrows - 1;
