@@ -237,7 +237,7 @@ __global__ void bc_step_faces_kernel(Geo g, Coef c, double* __restrict__ u, doub
 // wave's columns 1..126 (TENT_TWC per tile). Same expressions in the same
 // order as the reference loops, hence the same bits.
 #ifndef CFD_TENT_ALIGN
-#define CFD_TENT_ALIGN 0  // 1: tiles of 112 output columns starting on 128-B lines (lanes 4..59 store)
+#define CFD_TENT_ALIGN 1  // 1: tiles of 112 output columns starting on 128-B lines (lanes 4..59 store)
 #endif
 constexpr int TENT_TWC = CFD_TENT_ALIGN ? 112 : 126;
 #ifndef CFD_TENT_PD
