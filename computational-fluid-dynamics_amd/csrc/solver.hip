@@ -173,6 +173,7 @@ class Solver {
   double* resmax = nullptr;
   hipEvent_t ev_f0 = nullptr, ev_f1 = nullptr;
   int resident_lexw_waves = 2048;
+  int lexw_edge_pct = 100;  // wall-tile bands as long as interior ones (measured at 4096^2; CFD_LEXW_EDGE_PCT)
   bool use_lexw() const { return P.ordering == CFD_ORDER_LEX && P.case_id == CFD_CAVITY; }
   int lexw_ns() const { return P.sweeps_per_launch >= 1 ? P.sweeps_per_launch : 2; }
 
@@ -241,6 +242,7 @@ class Solver {
         resident_lexw_waves = std::max(1, std::min(lps, 4)) * 4 * prop.multiProcessorCount;
         // tuning: tiles per launch (fewer = taller bands, less halo recompute)
         if (const char* e = std::getenv("CFD_LEXW_WAVES")) resident_lexw_waves = std::max(64, std::atoi(e));
+        if (const char* e = std::getenv("CFD_LEXW_EDGE_PCT")) lexw_edge_pct = std::max(10, std::min(100, std::atoi(e)));
       }
       if (const char* e = std::getenv("CFD_PAIR_EDGE_PCT")) pair_edge_pct = std::max(10, std::min(100, std::atoi(e)));
       if (const char* e = std::getenv("CFD_MARCH_MIN_TH")) march_min_th = std::max(1, std::atoi(e));  // tuning
@@ -557,7 +559,9 @@ class Solver {
   // rows, marched in groups of 10 over th + march_extra rows, so th + extra is
   // a multiple of 10. The two boundary column tiles march slower (masks):
   // shorter bands, pair_edge_pct % of the interior march.
-  PairPlan multi_plan(int lo0, int hi0, int lo1, int hi1, int waves, int n, int max_th = 1 << 30) const {
+  PairPlan multi_plan(int lo0, int hi0, int lo1, int hi1, int waves, int n, int max_th = 1 << 30,
+                      int edge_pct = -1) const {
+    if (edge_pct < 0) edge_pct = pair_edge_pct;
     PairPlan pl{};
     pl.ctiles = (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC;
     pl.lo0 = lo0; pl.hi0 = hi0; pl.lo1 = lo1; pl.hi1 = hi1;
@@ -572,14 +576,14 @@ class Solver {
       pl.th = std::max(1, std::min(rmax, ((rows + nb - 1) / nb + ex + 9) / 10 * 10 - ex));
       if (pl.th > max_th) {  // (lexw: one wave marches at most max_th rows)
         pl.th = max_th;
-        pl.the = std::max(8, std::min(rmax, (pl.th + ex) * pair_edge_pct / 100 - ex));
+        pl.the = std::max(8, std::min(rmax, (pl.th + ex) * edge_pct / 100 - ex));
         pl.nb0 = nbands(lo0, hi0, pl.th);
         pl.nb1 = nbands(lo1, hi1, pl.th);
         pl.nbe0 = nbands(lo0, hi0, pl.the);
         pl.nbe1 = nbands(lo1, hi1, pl.the);
         break;
       }
-      pl.the = std::max(8, std::min(rmax, (pl.th + ex) * pair_edge_pct / 100 - ex));
+      pl.the = std::max(8, std::min(rmax, (pl.th + ex) * edge_pct / 100 - ex));
       pl.nb0 = nbands(lo0, hi0, pl.th);
       pl.nb1 = nbands(lo1, hi1, pl.th);
       pl.nbe0 = nbands(lo0, hi0, pl.the);
@@ -872,7 +876,8 @@ class Solver {
     std::vector<PairPlan> plans(S.size());
     for (size_t q = 0; q < S.size(); ++q)
       plans[q] = multi_plan(S[q].g.wj0, S[q].g.wj1 + 1, 0, 0, resident_lexw_waves / (int)S.size(), ns,
-                            96);  // (a wave's march <= 118 rows: its iterations fit one 64-bit mask)
+                            96,  // (a wave's march <= 118 rows: its iterations fit one 64-bit mask)
+                            lexw_edge_pct);
     // steady launches: every cell active in every half-sweep of the launch and
     // of the previous one's last (nx+ny+1 <= H0 <= 2K-2NS+1, H0 = 2 + 2NS m)
     const int ms0 = (P.nx + P.ny - 1 + 2 * ns - 1) / (2 * ns), ms1 = floordiv(2 * K - 2 * ns - 1, 2 * ns);
