@@ -643,6 +643,10 @@ struct WaveCtx {
   const double* f;
   int gi, gic, y0, y1, rmin, rmax;
   int py0 = 0, py1 = 0;  // proof mode: rows [py0, py1) whose black cells prove (band rows, 1 <= j < ny)
+  // step, interior path over the solid block's lower edge (row-uniform
+  // geometry): rows >= uhi are solid (never updated), row blk_row (the first
+  // solid row) is refreshed from the fluid row below, residuals up to res_hi
+  int uhi = 1 << 30, blk_row = -1, res_hi = 1 << 30;
   // cavity boundary-column waves: the reference's indicator products as lane
   // constants (eps_e, eps_w as 1.0 / 0.0; x * 0.0 == copysign(0, x), the
   // reference's 0 * x, for finite x) and omega / neighbour_count below / at
@@ -980,7 +984,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     if ((APAR == 2) ? ((j & 1) == 0) : ((APAR ^ 1) == 0)) {  // APAR 2: parity known at run time only
       const double Lb = dpp_from_left(m.y);
       if (FAST) {
-        if (!RC || (j > x.rmin && j < x.rmax)) m.x = sor_fast<CASE>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
+        if (!RC || (j > x.rmin && j < x.rmax && j < x.uhi)) m.x = sor_fast<CASE>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_red.x);
@@ -989,7 +993,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     } else {
       const double Ra = dpp_from_right(m.x);
       if (FAST) {
-        if (!RC || (j > x.rmin && j < x.rmax)) m.y = sor_fast<CASE>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
+        if (!RC || (j > x.rmin && j < x.rmax && j < x.uhi)) m.y = sor_fast<CASE>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_red.y);
@@ -1004,7 +1008,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     if ((APAR == 2) ? ((j & 1) == 1) : (APAR == 1)) {
       const double Lb = dpp_from_left(m.y);
       if (FAST) {
-        if (!RC || (j > x.rmin && j < x.rmax)) m.x = sor_fast<CASE>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
+        if (!RC || (j > x.rmin && j < x.rmax && j < x.uhi)) m.x = sor_fast<CASE>(x, j, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_black.x);
@@ -1013,7 +1017,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     } else {
       const double Ra = dpp_from_right(m.x);
       if (FAST) {
-        if (!RC || (j > x.rmin && j < x.rmax)) m.y = sor_fast<CASE>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
+        if (!RC || (j > x.rmin && j < x.rmax && j < x.uhi)) m.y = sor_fast<CASE>(x, j, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
       } else {
         const double nv =
             sor_update<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_black.y);
@@ -1038,6 +1042,10 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
       }
       if (j == 0) nv = wn;       // p[0][i] = p[1][i]
       if (j == ny + 1) nv = ws;  // p[ny+1][i] = p[ny][i]
+      if (CASE == BACKSTEP && j == x.blk_row) {  // backwards_step-01.cpp:708-738: one fluid neighbour (S),
+        nv.x = 0.0 + ws.x;                       // the average (0 + p_S) / 1 of the reference
+        nv.y = 0.0 + ws.y;
+      }
     }
     if (CASE != CAVITY && !FAST) {
       const int j = A - 3 * DIR;
@@ -1067,7 +1075,7 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
 #endif
       }
       if (FAST) {
-        if (!RC || (j >= x.g.j0 && j <= x.g.j1)) {  // row-uniform
+        if (!RC || (j >= x.g.j0 && j <= x.g.j1 && j <= x.res_hi)) {  // row-uniform
           if (CASE == CAVITY && j == ny) {  // top row: eps_n = 0 (cavity-01.cpp:666)
             rm = fmax(rm, residual_abs<CASE>(c, nx, ny, j, x.gi, m.x, Lb, m.y, CFD_S(bh.x, ah.x), CFD_N(bh.x, ah.x), f_res.x));
             rm = fmax(rm, residual_abs<CASE>(c, nx, ny, j, x.gi + 1, m.y, m.x, Ra, CFD_S(bh.y, ah.y), CFD_N(bh.y, ah.y), f_res.y));
@@ -1519,7 +1527,14 @@ struct PairPlan {
   int th, nb0, nb1;    // interior column tiles: band height, bands in range 0 / 1
   int the, nbe0, nbe1; // boundary column tiles
   int lo0, hi0, lo1, hi1;
+  int cxa, cxb;        // step: column tiles across the step's column (+1; 0: none), banded like the boundary ones
 };
+
+// column tiles banded as boundary tiles (masked march): the first and last,
+// and the step's mixed ones
+__host__ __device__ inline int plan_edge_tiles(const PairPlan& pl) {
+  return (pl.ctiles >= 2 ? 2 : 1) + (pl.cxa > 0) + (pl.cxb > 0);
+}
 
 // PROOF (cavity): the convergence test of each sweep is the proof above
 // instead of the max-norm residual; the fields are the same bits.
@@ -1557,16 +1572,18 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
   const int blk = ((flags & 2) && bl < L8) ? (bl % 8) * (nblk / 8) + bl / 8 : bl;
   const int tile = blk * 4 + wv;
   const int ne = (pl.ctiles >= 2) ? 2 : 1;
+  const int ned = plan_edge_tiles(pl);
   const int nbe = pl.nbe0 + pl.nbe1, nbi = pl.nb0 + pl.nb1;
   int band, ctile, th, nb0;
-  if (tile < ne * nbe) {
-    ctile = (tile < nbe) ? 0 : pl.ctiles - 1;
+  if (tile < ned * nbe) {
+    const int e = tile / nbe;  // boundary tiles 0 / last, then the step's mixed ones
+    ctile = (e == 0) ? 0 : (e == 1 && ne == 2) ? pl.ctiles - 1 : (e == ne && pl.cxa > 0) ? pl.cxa - 1 : pl.cxb - 1;
     band = tile % nbe;
     th = pl.the;
     nb0 = pl.nbe0;
   } else {
-    const int t = tile - ne * nbe;
-    const int nci = pl.ctiles - ne;
+    const int t = tile - ned * nbe;
+    const int nci = pl.ctiles - ned;
     if (t >= nci * nbi) return;
     if (flags & 64) {  // band-minor order (diagnostic)
       ctile = 1 + t / nbi;
@@ -1576,6 +1593,9 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
       ctile = 1 + t % nci;
       band = t / nci;
     }
+    // skip the mixed tiles (cxa < cxb, both inside 1 .. ctiles-2)
+    if (pl.cxa > 0 && ctile >= pl.cxa - 1) ++ctile;
+    if (pl.cxb > 0 && ctile >= pl.cxb - 1) ++ctile;
     th = pl.th;
     nb0 = pl.nb0;
   }
@@ -1610,6 +1630,15 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
     // or refreshed (both buffers hold its values): nothing to do
     if (y1 + 10 <= c.inlet_jmax - 1) cols_in = true;
     else if (y0 - 10 >= c.inlet_jmax + 2 && y1 + 10 <= g.ny && c0 + 128 <= c.step_i - 1) return;
+    else if (c0 + 128 <= c.step_i - 1 && y0 - 10 >= 1 && y1 + 10 <= g.ny) {
+      // a band across the block's lower edge, every column inside the block:
+      // fluid below, solid above, row-uniform - the interior path with the
+      // edge row rules (WaveCtx uhi / blk_row / res_hi), not per-cell masks
+      cols_in = true;
+      x.uhi = c.inlet_jmax + 1;
+      x.blk_row = c.inlet_jmax + 1;
+      x.res_hi = c.inlet_jmax;
+    }
   }
   const bool up = CFD_CAV_UP && (flags & 1) && (band & 1);
   // interior band whose march (rows y0 - 2NS - 2 .. y1 + 2NS + 1: the
@@ -1648,7 +1677,7 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
     if (fast) {
       // bands whose march (rows y0 - 9 .. y1 + 8) stays off the ghost rows:
       // no row checks, no refresh
-      const bool osafe = y0 - (PAIR_H + 2) > x.rmin && y1 + (PAIR_H + 2) < min(x.rmax, g.ny + 1);
+      const bool osafe = x.blk_row < 0 && y0 - (PAIR_H + 2) > x.rmin && y1 + (PAIR_H + 2) < min(x.rmax, g.ny + 1);
       if (osafe && up) wave_march_pair<CASE, -1, true, false>(x, y0, y1, r1, r2);
       else if (osafe) wave_march_pair<CASE, 1, true, false>(x, y0, y1, r1, r2);
       else if (up) wave_march_pair<CASE, -1, true>(x, y0, y1, r1, r2);

@@ -127,13 +127,7 @@ class Solver {
   int sweeps_per_launch() const {
     if (P.sweeps_per_launch == 1) return 1;
     if (P.sweeps_per_launch == 2) return 2;
-    if (P.case_id == CFD_CAVITY) return 3;
-    // backwards step on one process: the single-sweep march matches the pair
-    // launch's throughput (8192x512: 32.1 us per sweep vs 66.0 per pair) with
-    // half the halo rows; ranks keep pairs (one exchange and all-reduce per
-    // two sweeps, overlapped)
-    if (P.case_id == CFD_BACKSTEP && !comm) return 1;
-    return 2;
+    return P.case_id == CFD_CAVITY ? 3 : 2;
   }
   struct LaunchRec {
     int first, n;        // iterations first .. first+n-1
@@ -571,8 +565,21 @@ class Solver {
     PairPlan pl{};
     pl.ctiles = (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC;
     pl.lo0 = lo0; pl.hi0 = hi0; pl.lo1 = lo1; pl.hi1 = hi1;
+    if (P.case_id == CFD_BACKSTEP) {
+      // interior column tiles across the step's column (neither left of it,
+      // kernels.hpp: c0 + 128 <= step_i - 1, nor right, c0 > step_i + 1) march
+      // with per-cell masks: band them like the boundary tiles
+      int nx_found = 0;
+      for (int ct = 1; ct + 1 < pl.ctiles && nx_found < 2; ++ct) {
+        const int c0 = ct * PAIR_TWC - 8;
+        if (!(c0 > C.step_i + 1) && !(c0 + 128 <= C.step_i - 1)) {
+          (nx_found == 0 ? pl.cxa : pl.cxb) = ct + 1;
+          ++nx_found;
+        }
+      }
+    }
     const int rows = (hi0 - lo0) + (hi1 - lo1);
-    const int ne = pl.ctiles >= 2 ? 2 : 1;
+    const int ne = plan_edge_tiles(pl);
     const int rmax = std::max(hi0 - lo0, hi1 - lo1);
     const int ex = march_extra(n);
     auto nbands = [](int lo, int hi, int t) { return hi > lo ? (hi - lo + t - 1) / t : 0; };
@@ -608,7 +615,7 @@ class Solver {
     // bit 2: no test at all (the solve has already stopped); bit 7: the tested
     // window holds proof ratios (it was computed by a proof-mode launch)
     const int fl = march_flags | (replay ? 4 : 0) | (window_proof ? 128 : 0);
-    const int ne = pl.ctiles >= 2 ? 2 : 1;
+    const int ne = plan_edge_tiles(pl);
     const int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
     if (ntiles == 0) return;
     const dim3 grid((ntiles + 3) / 4);
