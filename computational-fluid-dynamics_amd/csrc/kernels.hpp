@@ -438,6 +438,42 @@ __global__ __launch_bounds__(256) void source_kernel(Geo g, Coef c, const double
   }
 }
 
+// Cavity source term + max|f| (cavity-01.cpp:622-630) on column pairs: a
+// wave covers 128 columns of one row with 16-B loads and stores (u* of column
+// i-1 by DPP; lane 0 loads it), a block 4 rows. Same expression per cell as
+// source_kernel, hence the same bits; the open cases keep source_kernel (their
+// mean's block-partial order).
+__global__ __launch_bounds__(256) void cavity_source_kernel(Geo g, Coef c, const double* __restrict__ us,
+                                                            const double* __restrict__ vs, double* __restrict__ f,
+                                                            double* __restrict__ srcmax) {
+  const int lane = threadIdx.x & 63;
+  const int gi = blockIdx.x * 128 + 2 * lane;  // even: the pair (gi, gi + 1) is 16-B aligned (pitch % 16 == 0)
+  const int j = max(g.j0, 1) + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int nx = g.nx;
+  double m = 0.0;
+  if (j <= min(g.j1, g.ny) && gi <= nx) {  // (lanes past nx idle; a lane's left neighbour is active)
+    const size_t o = at(g, j, gi), P = (size_t)g.pitch;
+    const double2 uc = *reinterpret_cast<const double2*>(us + o);
+    const double2 vc = *reinterpret_cast<const double2*>(vs + o);
+    const double2 vm = *reinterpret_cast<const double2*>(vs + o - P);
+    double uw = dpp_from_left(uc.y);
+    if (lane == 0) uw = us[o - 1];  // (gi = 0: row j-1's last value, unused)
+    const double dua = uc.x - uw, dub = uc.y - uc.x;
+    const double dva = vc.x - vm.x, dvb = vc.y - vm.y;
+    const double fa = c.cav_src * (dua * c.idx + dva * c.idx);
+    const double fb = c.cav_src * (dub * c.idx + dvb * c.idx);
+    const bool out_a = gi >= 1, out_b = gi + 1 <= nx;
+    if (out_a && out_b) {
+      *reinterpret_cast<double2*>(f + o) = make_double2(fa, fb);
+    } else {
+      if (out_a) f[o] = fa;
+      if (out_b) f[o + 1] = fb;
+    }
+    m = fmax(out_a ? fabs(fa) : 0.0, out_b ? fabs(fb) : 0.0);
+  }
+  block_max_to_shard<256>(m, srcmax, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
+}
+
 // Sum of per-block partials in a fixed order (one block).
 __global__ __launch_bounds__(256) void sum_partials_kernel(const double* __restrict__ partials, int n,
                                                            double* __restrict__ out) {

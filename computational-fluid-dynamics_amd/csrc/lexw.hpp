@@ -505,15 +505,28 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
 #undef LX_S10
 
 // max-norm residual of a cavity field (cavity-01.cpp:659-677) over the owned
-// interior cells: the residual the reference reports after its last sweep
+// interior cells: the residual the reference reports after its last sweep.
+// Column pairs like cavity_source_kernel: a wave covers 128 columns of one
+// row with 16-B loads, row neighbours by DPP (lanes 0 / 63 load theirs).
 __global__ __launch_bounds__(256) void cavity_resmax_kernel(Geo g, Coef c, const double* __restrict__ p,
                                                             const double* __restrict__ f, double* __restrict__ shards) {
-  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int j = g.j0 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int gi = blockIdx.x * 128 + 2 * lane;  // even: 16-B aligned pair
+  const int j = max(g.j0, 1) + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int nx = g.nx, ny = g.ny;
   double m = 0.0;
-  if (i >= 1 && i <= g.nx && j >= 1 && j <= g.ny && j <= g.j1) {
-    const size_t o = at(g, j, i), P = (size_t)g.pitch;
-    m = residual_abs<CAVITY>(c, g.nx, g.ny, j, i, p[o], p[o - 1], p[o + 1], p[o - P], p[o + P], f[o]);
+  if (j <= min(g.j1, ny) && gi <= nx) {  // (a lane's left neighbour is active)
+    const size_t o = at(g, j, gi), P = (size_t)g.pitch;
+    const double2 pc = *reinterpret_cast<const double2*>(p + o);
+    const double2 ps = *reinterpret_cast<const double2*>(p + o - P);
+    const double2 pn = *reinterpret_cast<const double2*>(p + o + P);
+    const double2 fc = *reinterpret_cast<const double2*>(f + o);
+    double pw = dpp_from_left(pc.y), pe = dpp_from_right(pc.x);
+    if (lane == 0) pw = p[o - 1];
+    if (lane == 63 || gi + 2 > nx) pe = p[o + 2];  // (the right neighbour lane idles past nx; o + 2 <= nx + 2 < pitch)
+    const double ra = residual_abs<CAVITY>(c, nx, ny, j, gi, pc.x, pw, pc.y, ps.x, pn.x, fc.x);
+    const double rb = residual_abs<CAVITY>(c, nx, ny, j, gi + 1, pc.y, pc.x, pe, ps.y, pn.y, fc.y);
+    m = fmax(gi >= 1 ? ra : 0.0, gi + 1 <= nx ? rb : 0.0);
   }
   block_max_to_shard<256>(m, shards, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
 }

@@ -490,7 +490,7 @@ class Solver {
       exchange(B_V, 1);
     }
     for (auto& s : S) {
-      const int ct = (P.nx + TENT_TWC - 1) / TENT_TWC, rows = s.g.j1 - s.g.j0 + 1;
+      const int ct = P.nx / TENT_TWC + 1, rows = s.g.j1 - s.g.j0 + 1;
       static const int tth = std::getenv("CFD_TENT_TH") ? std::max(4, std::atoi(std::getenv("CFD_TENT_TH"))) : 64;
       const int th = std::max(1, std::min(tth, rows));  // rows per band (tuned: 64)
       const int tiles = ct * ((rows + th - 1) / th);
@@ -499,13 +499,24 @@ class Solver {
     }
   }
 
+  // grid of the cavity's column-pair passes (cavity_source_kernel,
+  // cavity_resmax_kernel): 128 columns x 4 owned interior rows per block
+  dim3 pair_grid(const Strip& s) const {
+    const int rows = std::min(s.g.j1, P.ny) - std::max(s.g.j0, 1) + 1;
+    return dim3(P.nx / 128 + 1, std::max(1, (rows + 3) / 4));
+  }
+
   bool srcmax_ready = false;  // srcmax holds max|f| of the current source (reduced by the source passes)
 
   void build_source() {
     HIPC(hipMemsetAsync(srcmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
     if (multi()) exchange(B_VS, 1);
     for (auto& s : S) {
-      source_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_US], s.b[B_VS], s.b[B_F], partials + s.part_off, srcmax);
+      if (P.case_id == CFD_CAVITY) {
+        cavity_source_kernel<<<pair_grid(s), 256, 0, st>>>(s.g, C, s.b[B_US], s.b[B_VS], s.b[B_F], srcmax);
+      } else {
+        source_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_US], s.b[B_VS], s.b[B_F], partials + s.part_off, srcmax);
+      }
       check_launch("source");
     }
     if (P.case_id != CFD_CAVITY) {
@@ -1020,7 +1031,7 @@ class Solver {
       if (multi()) exchange(bp, 1);
       HIPC(hipMemsetAsync(resmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
       for (auto& s : S) {
-        cavity_resmax_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_F], resmax);
+        cavity_resmax_kernel<<<pair_grid(s), 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_F], resmax);
         check_launch("cavity_resmax");
       }
       HIPC(hipMemcpyAsync(h_shard, resmax, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -1100,7 +1111,7 @@ class Solver {
     if (multi()) exchange(bp, 1);
     HIPC(hipMemsetAsync(resmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
     for (auto& s : S) {
-      cavity_resmax_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_F], resmax);
+      cavity_resmax_kernel<<<pair_grid(s), 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_F], resmax);
       check_launch("cavity_resmax");
     }
     if (comm && comm->nranks > 1) comm_allreduce_max(comm, resmax, RES_SHARDS * SHARD_STRIDE, st);

@@ -14,7 +14,7 @@ for lib in ${LIBS:-default}; do
     env $(echo "$e" | tr "," " ") CFD_AMD_LIB=$L timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $D -o run --output-format csv -- python3 bench.py --steps 4 --warmup 1 --max-iters 6 --no-cpu-baseline --lex-steps 0 > $D.out 2> $D.err
     rc=$?
     [ $rc -ne 0 ] && { echo "run $n ($lib $e) exit $rc"; tail -3 $D.err; exit $rc; }
-    echo "[$lib $e]"; grep -E "tentative|source_kernel|correct_kernel|centers_stats|subtract_mean|bc_cavity" $D/run_kernel_stats.csv | awk -F',' '{gsub(/"/,"",$1); split($1,a,"("); printf "  %-40s %s\n", a[1], $4}'
+    echo "[$lib $e]"; grep -E "tentative|source_kernel|resmax|correct_kernel|centers_stats|subtract_mean|bc_cavity" $D/run_kernel_stats.csv | awk -F',' '{gsub(/"/,"",$1); split($1,a,"("); printf "  %-40s %s\n", a[1], $4}'
     n=$((n+1))
   done
 done

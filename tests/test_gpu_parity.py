@@ -286,3 +286,35 @@ def test_log_lines_match_reference_format():
         assert len(fa) == len(fb) and fa[0] == fb[0] and fa[1] == fb[1]
         ka, kb = float(fa[3].split("=")[1]), float(fb[3].split("=")[1])
         assert abs(ka - kb) <= 1.5e-6
+
+
+@pytest.mark.parametrize("strips", [1, 2])
+@pytest.mark.parametrize("nx", [111, 112, 113, 224, 300])
+def test_cavity_column_tile_widths(nx, strips):
+    """The cavity's column-tiled passes (tentative_kernel: 112-column tiles;
+    cavity_source_kernel + max|f|: 128-column pairs) at widths on and next to
+    a tile edge, bit-exact vs the oracle. ny = 190 keeps the grid off the
+    one-workgroup path; a capped solve in each ordering checks the tolerance
+    (from max|f|) and the reported residual."""
+    ny = 190
+    for ordering, oo in (("rb", O.RB), ("lex", O.LEX)):
+        cp = C.make_params("cavity", re=100.0, nx=nx, ny=ny, dt=1e-3, max_iters=40)
+        g = C.solver_for(cp, n_strips=strips, ordering=ordering)
+        o = O.Oracle(cp, ordering=oo)
+        rng = np.random.default_rng(nx * 10 + strips)
+        set_both(g, o, "u", rng.standard_normal((ny + 2, nx + 1)), cp)
+        set_both(g, o, "v", rng.standard_normal((ny + 1, nx + 2)), cp)
+        g.applyBoundaryConditions()
+        o.velocity_bc(False)
+        g.computeTentativeVelocities()
+        o.tentative()
+        assert_bits(g.field("us"), ofield(o, "us", cp), "tentative u*")
+        assert_bits(g.field("vs"), ofield(o, "vs", cp), "tentative v*")
+        g.buildSourceTerm()
+        o.source()
+        assert_bits(g.field("src"), o.field("src"), "source")
+        it_g, res_g = g.solverPressurePoisson()
+        it_o, res_o = o.poisson()
+        assert (it_g, res_g) == (it_o, res_o), ordering
+        assert_bits(g.field("p"), o.field("p"), f"pressure ({ordering})")
+        g.close()
