@@ -10,9 +10,9 @@ All inputs are device-resident when the timed region starts.
   value = interior cells x SOR iterations summed over all ranks / wall time of
           the K timed steps (max over ranks), in MLUPS.
 
-Extra fields: steps_per_sec, roofline (the fused red-black SOR kernel, three
-sweeps per launch for the cavity: HIP events on the solver's stream over the
-timed region; `achieved` = the 24 B/cell one launch must move / launch time,
+Extra fields: steps_per_sec, roofline (the fused red-black SOR kernel, four
+sweeps per launch for the cavity with the proof-mode convergence test, three
+with exact residuals: HIP events on the solver's stream over the timed region; `achieved` = the 24 B/cell one launch must move / launch time,
 `effective_sweep_*` the same per sweep), cpu_baseline (the oracle's
 lexicographic SOR loop — the reference's loop restated in C — on a bounded
 sample of the same grid, rank 0 only), reference_order (N=1: the same
@@ -156,7 +156,10 @@ def main() -> int:
     ap.add_argument("--check-every", type=int, default=1,
                     help="residual test every N SOR iterations (1 = the reference's stop rule, at every GPU count)")
     ap.add_argument("--sweeps-per-launch", type=int, default=0,
-                    help="red-black SOR iterations fused per kernel launch (0: auto = 3 for the cavity)")
+                    help="SOR iterations fused per kernel launch (0: auto = 4 for the red-black cavity's "
+                         "proof-mode launches, 3 for exact-residual ones, 2 for the open cases)")
+    ap.add_argument("--proof-test", default="auto", choices=["auto", "off"],
+                    help="red-black cavity: proof-mode convergence test (off: exact residual every sweep)")
     ap.add_argument("--ordering", default="rb", choices=["rb", "lex"],
                     help="SOR sweep order: rb (red-black) or lex (the reference's lexicographic order, bit-identical)")
     ap.add_argument("--lex-steps", type=int, default=2,
@@ -199,10 +202,12 @@ def main() -> int:
         comm_info = _comm_info(comm)
         rows = strip_rows(rank, world, ny_global) if strong else weak_rows(rank, args.ny)
         solver = C.solver_for(cp, device=local_rank, check_every=check_every, rank_rows=rows, comm=comm,
-                              sweeps_per_launch=args.sweeps_per_launch, ordering=args.ordering)
+                              sweeps_per_launch=args.sweeps_per_launch, ordering=args.ordering,
+                              proof_test=args.proof_test)
     else:
         solver = C.solver_for(cp, device=local_rank, check_every=check_every,
-                              sweeps_per_launch=args.sweeps_per_launch, ordering=args.ordering)
+                              sweeps_per_launch=args.sweeps_per_launch, ordering=args.ordering,
+                              proof_test=args.proof_test)
 
     def barrier():
         if world > 1:
@@ -258,10 +263,10 @@ def main() -> int:
             traffic = pmc_traffic("r2_lexw_pmc.json", cp.nx, wrows, round(sweeps_per_launch))
         mlups = updates / elapsed / 1e6
         kcase = kcase_of(args.case)
-        # red-black cavity 3-sweep launches: proof-mode convergence test
-        # (CFD_PROOF=0 evaluates the residual in every sweep)
+        # red-black cavity launches: proof-mode convergence test (DESIGN.md
+        # §2; --proof-test off evaluates the residual in every sweep)
         proof = (not lexw and kcase == "cavity" and round(sweeps_per_launch) >= 3
-                 and os.environ.get("CFD_PROOF", "1") != "0")
+                 and args.proof_test != "off")
         if proof:
             traffic = pmc_traffic(f"r2_proof{round(sweeps_per_launch)}_pmc.json", cp.nx, wrows,
                                   round(sweeps_per_launch))

@@ -40,10 +40,14 @@ class CfdParams(ctypes.Structure):
         ("ra", ctypes.c_double), ("pr", ctypes.c_double), ("kappa", ctypes.c_double), ("buoyancy", ctypes.c_double),
         ("t_hot", ctypes.c_double), ("t_cold", ctypes.c_double), ("t_ref", ctypes.c_double),
         ("t_perturb", ctypes.c_double),
+        ("proof_test", ctypes.c_int), ("small_solve", ctypes.c_int), ("overlap", ctypes.c_int),
     ]
 
 
 ORDER = {"rb": 0, "lex": 1}
+SWITCH = {"auto": 0, "on": 1, "off": 2}  # enum cfd_switch
+TUNING = {"pair_wps": 0, "wave_wps": 1, "lexw_waves": 2, "lexw_edge_pct": 3, "pair_edge_pct": 4,
+          "march_min_th": 5, "tent_th": 6}  # enum cfd_tuning
 
 
 class StepInfo(ctypes.Structure):
@@ -95,6 +99,7 @@ SIGNATURES = {
     "cfd_get_timing": (_i, [_vp, ctypes.POINTER(Timing)]),
     "cfd_reset_timing": (_i, [_vp]),
     "cfd_synchronize": (_i, [_vp]),
+    "cfd_set_tuning": (_i, [_vp, _i, _i]),
     "cfd_comm_unique_id": (_i, [ctypes.POINTER(ctypes.c_ubyte)]),
     "cfd_comm_init": (_vp, [ctypes.POINTER(ctypes.c_ubyte), _i, _i, _i]),
     "cfd_comm_destroy": (_i, [_vp]),

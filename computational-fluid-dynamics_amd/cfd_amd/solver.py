@@ -20,14 +20,17 @@ from .params import BACKSTEP, CASE_NAMES, CAVITY, CHANNEL, RAYLEIGH_BENARD, Case
 
 
 def to_cparams(cp: CaseParams, check_every: int = 1, chunk: int = 0, ordering: str = "rb",
-               sweeps_per_launch: int = 0) -> _lib.CfdParams:
-    """Derived reference constants -> the C-ABI parameter block."""
+               sweeps_per_launch: int = 0, proof_test: str = "auto", small_solve: str = "auto",
+               overlap: str = "auto") -> _lib.CfdParams:
+    """Derived reference constants -> the C-ABI parameter block. proof_test /
+    small_solve / overlap: "auto", "on" or "off" (enum cfd_switch; they choose
+    how a solve runs, never its result bits)."""
     return _lib.CfdParams(
         cp.case_id, cp.nx, cp.ny, cp.length, cp.height, cp.re, cp.u_ref, cp.rho, cp.cfl, cp.final_time,
         cp.dx, cp.dy, cp.nu, cp.dt, cp.omega, cp.tol_factor, cp.abs_tol, cp.max_iters, cp.total_steps,
         cp.print_interval, cp.save_interval, cp.h_inlet, cp.step_x, cp.step_i, cp.inlet_jmax, check_every, chunk,
         _lib.ORDER[ordering], sweeps_per_launch, cp.ra, cp.pr, cp.kappa, cp.buoyancy, cp.t_hot, cp.t_cold,
-        cp.t_ref, cp.t_perturb)
+        cp.t_ref, cp.t_perturb, _lib.SWITCH[proof_test], _lib.SWITCH[small_solve], _lib.SWITCH[overlap])
 
 
 class _SolverBase:
@@ -37,16 +40,20 @@ class _SolverBase:
 
     def __init__(self, params: CaseParams | None = None, *, device: int = 0, n_strips: int = 1,
                  check_every: int = 1, chunk: int = 0, rank_rows: tuple[int, int] | None = None, comm=None,
-                 ordering: str = "rb", sweeps_per_launch: int = 0):
+                 ordering: str = "rb", sweeps_per_launch: int = 0, proof_test: str = "auto",
+                 small_solve: str = "auto", overlap: str = "auto", tuning: dict[str, int] | None = None):
         """ordering: "rb" (red-black SOR, the fast default) or "lex" (the reference's
-        lexicographic sweep, bit-identical to it; one device, one strip).
-        sweeps_per_launch: red-black iterations fused per kernel launch (0 = auto: 3
-        for the cavity, 2 otherwise; 1, 2, or 3 for the cavity); bit-identical
-        either way."""
+        lexicographic sweep, bit-identical to it; one device).
+        sweeps_per_launch: SOR iterations fused per kernel launch (0 = auto: red-black
+        cavity 4 in proof-mode launches and 3 in exact ones, 2 for the open cases;
+        lexicographic 3); bit-identical either way.
+        proof_test / small_solve / overlap: "auto" / "on" / "off" (include/cfd_amd.h).
+        tuning: launch-planning knobs (_lib.TUNING names), performance only."""
         self.params = params if params is not None else make_params(self.CASE)
         if self.params.case_id != self.CASE:
             raise ValueError(f"{type(self).__name__} needs case {CASE_NAMES[self.CASE]}")
-        self._cp = to_cparams(self.params, check_every, chunk, ordering, sweeps_per_launch)
+        self._cp = to_cparams(self.params, check_every, chunk, ordering, sweeps_per_launch, proof_test,
+                              small_solve, overlap)
         L = _lib.lib()
         if rank_rows is None:
             self._h = L.cfd_create(ctypes.byref(self._cp), device, n_strips)
@@ -54,6 +61,12 @@ class _SolverBase:
             self._h = L.cfd_create_rank(ctypes.byref(self._cp), device, rank_rows[0], rank_rows[1], comm)
         if not self._h:
             raise _lib.CfdError("cfd_create failed: " + L.cfd_last_error().decode(errors="replace"))
+        for knob, value in (tuning or {}).items():
+            self.set_tuning(knob, value)
+
+    def set_tuning(self, knob: str, value: int) -> None:
+        """cfd_set_tuning: a launch-planning knob (performance only, same bits)."""
+        _lib.check(_lib.lib().cfd_set_tuning(self._h, _lib.TUNING[knob], int(value)), "cfd_set_tuning")
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -26,6 +26,12 @@ constexpr int HALO = 8;           // halo rows stored per side (a fused pair of 
 constexpr int RES_SHARDS = 32;    // residual / max accumulators, one 128-B line each
 constexpr int SHARD_STRIDE = 16;  // doubles between shards (128 B)
 constexpr int RING = 16;          // residual ring slots (iteration k uses k & 15)
+// Slots a launch of iterations k..k+NS-1 clears for the next launch: k+NS ..
+// k+NS+RING_AHEAD-1, as many as the longest launch (4 sweeps). The farthest,
+// k+NS+3 = k+NS+3-16 mod RING, lies below every slot still read: the tested
+// window (at most two launches back, >= k-8) and this launch's own.
+constexpr int RING_AHEAD = 4;
+static_assert(4 + RING_AHEAD + 8 <= RING, "ring too small for the tested window and the cleared slots");
 
 struct Geo {
   int nx, ny;      // global interior cells
@@ -894,8 +900,11 @@ __global__ __launch_bounds__(256, CFD_WAVE_MIN_WAVES) void poisson_wave_kernel(G
   // of an iteration already known to be the solve's last)
   if (!(flags & 4) && !window_go_on(ctl, ka, kb, lane, blockIdx.x == 0 && wv == 0, (flags & 128) != 0)) return;
 
-  if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS)
-    ctl.ring[(size_t)((k + 1) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
+  if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS) {  // the next launch's slots (RING_AHEAD)
+#pragma unroll
+    for (int q = 0; q < RING_AHEAD; ++q)
+      ctl.ring[(size_t)((k + 1 + q) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
+  }
 
   // XCD-aware block order; the 4 waves of a block take 4 adjacent bands
   const int nblk = (int)gridDim.x;
@@ -1596,9 +1605,13 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
 
   // convergence test of the iterations [ka, kb] (flags bit 2: none, a replay)
   if (!(flags & 4) && !window_go_on(ctl, ka, kb, lane, blockIdx.x == 0 && wv == 0, (flags & 128) != 0)) return;
-  if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS) {  // the next launch's residual slots
+  if (blockIdx.x == 0 && wv == 0 && lane < RES_SHARDS) {
+    // the next launch's residual slots: RING_AHEAD of them whatever this
+    // launch's sweep count, because the next launch may run more sweeps than
+    // this one (an exact 3-sweep launch followed by a 4-sweep proof-mode launch
+    // after a fallback): a slot it atomically maxes into must start at zero
 #pragma unroll
-    for (int q = 0; q < NS; ++q)
+    for (int q = 0; q < RING_AHEAD; ++q)
       ctl.ring[(size_t)((k + NS + q) & (RING - 1)) * RES_SHARDS * SHARD_STRIDE + lane * SHARD_STRIDE] = 0.0;
   }
 
@@ -1621,14 +1634,10 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
     const int t = tile - ned * nbe;
     const int nci = pl.ctiles - ned;
     if (t >= nci * nbi) return;
-    if (flags & 64) {  // band-minor order (diagnostic)
-      ctile = 1 + t / nbi;
-      band = t % nbi;
-    } else {  // column tiles of one band side by side: their shared halo columns
-              // are read at the same moment on the same XCD (one L2)
-      ctile = 1 + t % nci;
-      band = t / nci;
-    }
+    // column tiles of one band side by side: their shared halo columns are
+    // read at the same moment on the same XCD (one L2)
+    ctile = 1 + t % nci;
+    band = t / nci;
     // skip the mixed tiles (cxa < cxb, both inside 1 .. ctiles-2)
     if (pl.cxa > 0 && ctile >= pl.cxa - 1) ++ctile;
     if (pl.cxb > 0 && ctile >= pl.cxb - 1) ++ctile;
@@ -1681,9 +1690,7 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
   // dependency cone and the pipeline's own rows) stays inside rows 1 .. ny-1:
   // no row checks (cav_update RC)
   const bool safe = y0 - (2 * NS + 2) > x.rmin && y1 + (2 * NS + 2) < min(x.rmax, g.ny);
-  // flags bit 4 / bit 5 (timing diagnostics only): never / always take the interior path
-  // (the proof needs four-neighbour cells: never forced onto the interior path)
-  const bool fast = PROOF ? cols_in : ((flags & 32) || (!(flags & 16) && cols_in));
+  const bool fast = cols_in;
   double r[NS];
   if constexpr (CASE == CAVITY) {  // the cavity's own pipeline (no refresh stage: depth 2NS+1)
     if constexpr (PROOF) {

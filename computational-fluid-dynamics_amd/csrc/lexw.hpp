@@ -70,7 +70,9 @@ struct LexCtl {
   int words;                 // per shard
   int kmax;                  // offset: bit of iteration k is k + kmax (>= 0 for every iteration a wave touches)
   const double* tol;         // [0] tolerance, [1] initial residual
-  int* stop;                 // [0] converged flag, [1] iteration
+  int* stop;                 // [0] 1: the reference stops at iteration [1]; 2: iteration [1] left open
+  int kexact;                // iterations >= kexact have every cell's residual evaluated (full
+                             // launches); below it the bits come from sampled rows (LX_SAMPLE)
 };
 
 // slot k has a cell whose |residual| exceeds the tolerance (valid once every
@@ -84,7 +86,9 @@ __device__ __forceinline__ bool lexw_slot_exceeds(const LexCtl& L, int k) {
 }
 
 // the reference's while condition for the slots [ka, kb] completed since the
-// last test (0 = the primed initial residual): false = stop (recorded once)
+// last test (0 = the primed initial residual): false = stop (recorded once).
+// A slot below kexact holds the sampled rows only: no exceedance there proves
+// nothing, the iteration is left open (stop code 2) for the host to evaluate.
 __device__ __forceinline__ bool lexw_go_on(const LexCtl& L, int ka, int kb, bool first_wave, int lane) {
   if (L.stop[0] != 0) return false;
   const double tol = L.tol[0];
@@ -93,7 +97,7 @@ __device__ __forceinline__ bool lexw_go_on(const LexCtl& L, int ka, int kb, bool
     if (!go) {
       if (first_wave && lane == 0) {
         L.stop[1] = k;
-        L.stop[0] = 1;
+        L.stop[0] = (k == 0 || k >= L.kexact) ? 1 : 2;
       }
       return false;
     }
@@ -231,7 +235,7 @@ __device__ __forceinline__ double lx_res(const WaveCtx<CAVITY>& x, double eN, in
 // ramp tiles, for cells outside the grid or inactive at H-1). Straight-line
 // code: branches on the row-uniform conditions split the march loop and
 // serialise its loads, so they become scalar coefficients and thresholds.
-template <int ROT, int JPAR, int COLOR, int MODE, bool EDGE, bool STORE>
+template <int ROT, int JPAR, int COLOR, int MODE, bool EDGE, bool STORE, bool RES>
 __device__ __forceinline__ void lx_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCol (&cc)[2],
                                        double2 (&W)[5], int j, int X, const LxAct& act, const double2& fc, int& exi) {
   double2& m = W[LX_SLOT(X)];
@@ -255,7 +259,9 @@ __device__ __forceinline__ void lx_row(const WaveCtx<CAVITY>& x, const LexCtx& l
     __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
   }
   // residual of the other colour's cell of this lane (iteration of half-sweep
-  // H-1), tested against +inf outside the wave's output rows
+  // H-1), tested against +inf outside the wave's output rows; RES = false:
+  // a row the sampled launch does not evaluate (lx_sweeps)
+  if constexpr (!RES) return;
   const bool rrow = j >= x.y0 && j < x.y1 && j >= x.g.j0 && j <= x.g.j1;  // row-uniform
   const double thr = rrow ? lc.tol : __builtin_huge_val();
   const double eN = top ? 0.0 : 1.0;
@@ -275,21 +281,33 @@ __device__ __forceinline__ void lx_row(const WaveCtx<CAVITY>& x, const LexCtx& l
   asm volatile("" : "+v"(exi));
 }
 
-template <int S, int NS, int ROT, int PAR, int MODE, bool EDGE>
+// Sampled residuals (MODE & LX_SAMPLE): the loop goes on iff SOME cell's
+// residual exceeds tol, so the exact residual of a subset of the cells proves
+// "go on" whenever one of them exceeds it. A sampled march evaluates the rows
+// j = Rbeg - 10q only: at step T of the 10-step unroll (front row R = Rbeg - T
+// - 10q) that is the row at X = T behind the front, a compile-time choice (one
+// residual row per step for T = 1 .. 2NS, none otherwise). An iteration whose
+// sampled rows all meet the tolerance is left open (LexCtl::kexact, stop
+// code 2) and evaluated exactly by the host (Solver::solve_lexw).
+constexpr int LX_SAMPLE = 2;
+template <int MODE, int T, int X>
+constexpr bool lx_res_row() { return !(MODE & LX_SAMPLE) || T == X; }
+
+template <int S, int NS, int T, int ROT, int PAR, int MODE, bool EDGE>
 __device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCol (&cc)[2],
                                           LexRun<NS>& s, int R, const LxAct& act, int& exi) {
   if constexpr (S < NS) {
     // red at R+2S+1 (parity PAR^1) in half-sweep H0+2S; black at R+2S+2 (PAR) in H0+2S+1
-    lx_row<ROT, PAR ^ 1, 0, MODE, EDGE, false>(x, lc, cc, s.w[S], R + 2 * S + 1, 2 * S + 1, act,
-                                               s.fr[LX_S10(2 * S + 1)], exi);
-    lx_row<ROT, PAR, 1, MODE, EDGE, S == NS - 1>(x, lc, cc, s.w[S], R + 2 * S + 2, 2 * S + 2, act,
-                                                 s.fr[LX_S10(2 * S + 2)], exi);
+    lx_row<ROT, PAR ^ 1, 0, MODE, EDGE, false, lx_res_row<MODE, T, 2 * S + 1>()>(
+        x, lc, cc, s.w[S], R + 2 * S + 1, 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi);
+    lx_row<ROT, PAR, 1, MODE, EDGE, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>()>(
+        x, lc, cc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi);
     if constexpr (S + 1 < NS) s.w[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
-    lx_sweeps<S + 1, NS, ROT, PAR, MODE, EDGE>(x, lc, cc, s, R, act, exi);
+    lx_sweeps<S + 1, NS, T, ROT, PAR, MODE, EDGE>(x, lc, cc, s, R, act, exi);
   }
 }
 
-template <int NS, int ROT, int PAR, int MODE, bool EDGE>  // PAR = parity of R
+template <int NS, int T, int ROT, int PAR, int MODE, bool EDGE>  // PAR = parity of R, T = step of the unroll
 __device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCol (&cc)[2],
                                         LexRun<NS>& s, int R, unsigned long long bit) {
   s.w[0][LX_SLOT(0)] = s.np[LX_SLOT(0)];
@@ -298,7 +316,8 @@ __device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& 
   s.nf[LX_SLOT(-4)] = lx_ld(x, x.f, R - 3);
   int exi = 0;
   const LxAct act = lx_act<MODE>(lc, x.gi, R);
-  lx_sweeps<0, NS, ROT, PAR, MODE, EDGE>(x, lc, cc, s, R, act, exi);
+  lx_sweeps<0, NS, T, ROT, PAR, MODE, EDGE>(x, lc, cc, s, R, act, exi);
+  if constexpr ((MODE & LX_SAMPLE) && (T < 1 || T > 2 * NS)) return;  // (no residual row at this step)
   s.mask |= exi ? bit : 0ull;
 }
 
@@ -356,16 +375,16 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
   // (nsteps + 9 <= 127 by the host's band limit: bits t/2 < 64)
 #define LX_BIT(T) ((((st + (T)) >> 1) < 64) ? (1ull << ((st + (T)) >> 1)) : 0ull)
   for (int st = 0; st < nsteps; st += 10, R -= 10) {
-    lx_step<NS, 0, 0, MODE, EDGE>(x, lc, cc, s, R, LX_BIT(0));
-    lx_step<NS, 1, 1, MODE, EDGE>(x, lc, cc, s, R - 1, LX_BIT(1));
-    lx_step<NS, 2, 0, MODE, EDGE>(x, lc, cc, s, R - 2, LX_BIT(2));
-    lx_step<NS, 3, 1, MODE, EDGE>(x, lc, cc, s, R - 3, LX_BIT(3));
-    lx_step<NS, 4, 0, MODE, EDGE>(x, lc, cc, s, R - 4, LX_BIT(4));
-    lx_step<NS, 0, 1, MODE, EDGE>(x, lc, cc, s, R - 5, LX_BIT(5));
-    lx_step<NS, 1, 0, MODE, EDGE>(x, lc, cc, s, R - 6, LX_BIT(6));
-    lx_step<NS, 2, 1, MODE, EDGE>(x, lc, cc, s, R - 7, LX_BIT(7));
-    lx_step<NS, 3, 0, MODE, EDGE>(x, lc, cc, s, R - 8, LX_BIT(8));
-    lx_step<NS, 4, 1, MODE, EDGE>(x, lc, cc, s, R - 9, LX_BIT(9));
+    lx_step<NS, 0, 0, 0, MODE, EDGE>(x, lc, cc, s, R, LX_BIT(0));
+    lx_step<NS, 1, 1, 1, MODE, EDGE>(x, lc, cc, s, R - 1, LX_BIT(1));
+    lx_step<NS, 2, 2, 0, MODE, EDGE>(x, lc, cc, s, R - 2, LX_BIT(2));
+    lx_step<NS, 3, 3, 1, MODE, EDGE>(x, lc, cc, s, R - 3, LX_BIT(3));
+    lx_step<NS, 4, 4, 0, MODE, EDGE>(x, lc, cc, s, R - 4, LX_BIT(4));
+    lx_step<NS, 5, 0, 1, MODE, EDGE>(x, lc, cc, s, R - 5, LX_BIT(5));
+    lx_step<NS, 6, 1, 0, MODE, EDGE>(x, lc, cc, s, R - 6, LX_BIT(6));
+    lx_step<NS, 7, 2, 1, MODE, EDGE>(x, lc, cc, s, R - 7, LX_BIT(7));
+    lx_step<NS, 8, 3, 0, MODE, EDGE>(x, lc, cc, s, R - 8, LX_BIT(8));
+    lx_step<NS, 9, 4, 1, MODE, EDGE>(x, lc, cc, s, R - 9, LX_BIT(9));
   }
 #undef LX_BIT
   // lane l's bit u <-> iteration Bd0 + u - l = (Bd0 - 63) + (u + 63 - l):
@@ -396,7 +415,7 @@ __host__ __device__ inline void lexw_rows(const Geo& g, int H0, int K, int ns, i
 // waves per SIMD); RAMP = true: the launches at the start and the end of the
 // solve, whose tiles take the masked marches unless wholly active (the masked
 // code would cost the steady kernel registers, so it lives in its own kernel).
-template <int NS, bool RAMP>
+template <int NS, bool RAMP, bool SAMPLE = false>
 __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisson_lexw_kernel(Geo g, Coef c, const double* __restrict__ pin,
                                                               double* __restrict__ pout, const double* __restrict__ f,
                                                               LexCtl L, int H0, int K, int ka, int kb, PairPlan pl,
@@ -488,16 +507,17 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   LexCtx lc{H0, K, L.tol[0], uni(c.om_nc[2]), uni(c.om_nc[3]), uni(c.om_nc[4])};
   const int shard = bl & (LEXW_SHARDS - 1);
   const bool edge = !cols_in;
+  constexpr int SM = SAMPLE ? LX_SAMPLE : 0;
   if constexpr (RAMP) {
     // tiles of a ramp launch whose every cell is active in every half-sweep
     // it evaluates (H0-1 .. H0+2NS-1) take the unmasked march
     const bool full = smax <= H0 - 2 && Hend <= smin + last;
-    if (edge) lx_march<NS, LX_ACT, true>(x, lc, L, y0, y1, c0, lane, shard);
-    else if (full) lx_march<NS, 0, false>(x, lc, L, y0, y1, c0, lane, shard);
-    else lx_march<NS, LX_ACT, false>(x, lc, L, y0, y1, c0, lane, shard);
+    if (edge) lx_march<NS, LX_ACT | SM, true>(x, lc, L, y0, y1, c0, lane, shard);
+    else if (full) lx_march<NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard);
+    else lx_march<NS, LX_ACT | SM, false>(x, lc, L, y0, y1, c0, lane, shard);
   } else {
-    if (edge) lx_march<NS, 0, true>(x, lc, L, y0, y1, c0, lane, shard);
-    else lx_march<NS, 0, false>(x, lc, L, y0, y1, c0, lane, shard);
+    if (edge) lx_march<NS, SM, true>(x, lc, L, y0, y1, c0, lane, shard);
+    else lx_march<NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard);
   }
 }
 

@@ -43,8 +43,13 @@ __global__ __launch_bounds__(SMALL_THREADS) void poisson_small_kernel(Geo g, Coe
                                                                       int check_every, int* __restrict__ out_iters,
                                                                       double* __restrict__ out_res) {
   __shared__ double P[SMALL_CELLS];
-  __shared__ unsigned long long rmax_slot[2];  // max|r| of the iteration (alternating slots)
-  __shared__ int proven[2];                    // proof-mode: some cell proved |r| > tol (alternating)
+  // per-iteration slots, rotating over three: iteration it uses slot it % 3 and
+  // clears slot (it + 1) % 3 after its red half-sweep. That slot's last reads
+  // were in iteration it - 2, and every wave has passed iteration it - 1's
+  // barriers since, so no wave can still read it (two slots would race: a
+  // lagging wave reading iteration it - 1's slot after thread 0 cleared it)
+  __shared__ unsigned long long rmax_slot[3];  // max|r| of the iteration
+  __shared__ int proven[3];                    // proof-mode: some cell proved |r| > tol
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int nx = g.nx, ny = g.ny, W = nx + 2;
   auto gidx = [&](int j, int i) { return (size_t)(j - g.row_lo) * (size_t)g.pitch + (size_t)i; };
@@ -102,7 +107,7 @@ __global__ __launch_bounds__(SMALL_THREADS) void poisson_small_kernel(Geo g, Coe
       }
     }
   }
-  if (t < 2) {
+  if (t < 3) {
     rmax_slot[t] = 0ull;
     proven[t] = 0;
   }
@@ -113,12 +118,13 @@ __global__ __launch_bounds__(SMALL_THREADS) void poisson_small_kernel(Geo g, Coe
   const bool proof = CASE == CAVITY && c.proof_k > 0.0;
   const double kc = c.proof_k * (1.0 - 0x1p-38);
   double res = tolv[1];  // the loop's primed value (cavity-01.cpp:618, channel-01.cpp:649)
-  int it = 0;
+  int it = 0, sl = 0;  // sl = it % 3
   __syncthreads();
   // cavity-01.cpp:635 / channel-01.cpp:652 / backwards_step-01.cpp:893
   while (res > tol && it < max_iters) {
     ++it;
-    const int sl = it & 1;
+    sl = (sl == 2) ? 0 : sl + 1;
+    const int sl_next = (sl == 2) ? 0 : sl + 1;
     // tested on check_every multiples and at the cap, like the multi-launch
     // solve; the cap always evaluates the residual (it is reported)
     const bool tested = it % check_every == 0 || it == max_iters;
@@ -152,9 +158,9 @@ __global__ __launch_bounds__(SMALL_THREADS) void poisson_small_kernel(Geo g, Coe
         }
       }
       if (col == 0) {
-        if (t == 0) {  // the next iteration's slots (their last readers are past this barrier)
-          rmax_slot[sl ^ 1] = 0ull;
-          proven[sl ^ 1] = 0;
+        if (t == 0) {  // the next iteration's slots (last read in iteration it - 2)
+          rmax_slot[sl_next] = 0ull;
+          proven[sl_next] = 0;
         }
       } else if (pf) {
         proven[sl] = 1;  // (any proving lane: the same value)

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 6
+#define CFD_AMD_ABI_VERSION 7
 
 /* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
  * tree (only figures): it is the cavity's projection step with a resting lid
@@ -71,15 +71,27 @@ typedef struct cfd_params {
   int ordering;         /* CFD_ORDER_RB (red-black, strips/ranks) or CFD_ORDER_LEX (the reference's
                            sweep order, bit-identical: cavity / Rayleigh-Benard at any size and in
                            strips on one device; channel / step on one workgroup, nx+ny < 12000) */
-  int sweeps_per_launch; /* SOR iterations fused into one kernel launch: 0 = auto (red-black: 3 for
-                           the cavity, 2 otherwise; lexicographic cavity: 2), 1, 2 or 3 (cavity);
-                           bit-identical either way */
+  int sweeps_per_launch; /* SOR iterations fused into one kernel launch, bit-identical for every value:
+                           0 = auto (red-black cavity: 4 in proof-mode launches, 3 in exact-residual
+                           ones; red-black channel / step: 2; lexicographic cavity: 3);
+                           1, 2; 3 (cavity: every launch 3); 4 (red-black cavity with the proof test:
+                           the auto plan, stated) */
   /* Rayleigh-Benard (case 3), free-fall units: H = 1, U = sqrt(g beta dT H),
    * nu = sqrt(Pr/Ra), kappa = 1/sqrt(Ra Pr); hot bottom wall t_hot, cold top
    * wall t_cold, adiabatic side walls; buoyancy (T - t_ref) on v. */
   double ra, pr, kappa, buoyancy, t_hot, t_cold, t_ref;
   double t_perturb;     /* initial T = conduction profile + t_perturb*sin(pi y)cos(pi x/L) */
+  /* Solve-path switches (enum cfd_switch; cfd_params_init sets CFD_AUTO). None of them changes a
+   * result bit (iteration counts, residuals, fields); they choose how the same solve runs. */
+  int proof_test;       /* red-black cavity: proof-mode convergence test where it applies
+                           (AUTO / ON); OFF: the max-norm residual in every tested sweep */
+  int small_solve;      /* red-black, one strip, no ranks, p fits the LDS: the whole solve in one
+                           workgroup (small.hpp) (AUTO / ON); OFF: the multi-launch solve */
+  int overlap;          /* ranks with >= 48 rows: halo exchange overlapped with the interior rows
+                           (AUTO / ON); OFF: exchange in front of each launch */
 } cfd_params;
+
+enum cfd_switch { CFD_AUTO = 0, CFD_ON = 1, CFD_OFF = 2 };
 
 enum cfd_ordering { CFD_ORDER_RB = 0, CFD_ORDER_LEX = 1 };
 
@@ -101,7 +113,7 @@ typedef struct cfd_timing {
   long long poisson_cell_updates; /* interior cells x active iterations (this rank) */
   double step_ms;             /* device time of whole timesteps */
   long long steps;
-  long long poisson_sweeps;   /* SOR iterations executed by those launches (up to 3 per fused launch) */
+  long long poisson_sweeps;   /* SOR iterations executed by those launches (up to 4 per fused launch) */
   long long poisson_overlapped; /* pair launches split into interior + halo-overlapped boundary rows (ranks) */
   double poisson_steady_ms;   /* lexicographic order: device time of the launches with every cell active */
   long long poisson_steady_launches; /* (the ramps at the start / end of a solve excluded) */
@@ -173,6 +185,19 @@ int cfd_write_vtk_arrays(const cfd_params* p, const char* filename, double time_
 
 /* Interior rows [first, last] (global, 1-based) this solver owns. */
 int cfd_owned_rows(const cfd_solver* s, int* first, int* last);
+
+/* Launch-planning knobs (performance only: every value gives the same bits).
+ * Defaults are the values measured best on MI355X. */
+enum cfd_tuning {
+  CFD_TUNE_PAIR_WPS = 0,      /* waves per SIMD the fused red-black launch is planned for (1..4) */
+  CFD_TUNE_WAVE_WPS = 1,      /* the same for the one-sweep launch */
+  CFD_TUNE_LEXW_WAVES = 2,    /* tiles per lexicographic-order launch (>= 64) */
+  CFD_TUNE_LEXW_EDGE_PCT = 3, /* wall-tile band length, % of the interior band (10..100) */
+  CFD_TUNE_PAIR_EDGE_PCT = 4, /* boundary-column band length of red-black launches, % (10..100) */
+  CFD_TUNE_MARCH_MIN_TH = 5,  /* minimum rows per band of a march launch (>= 1) */
+  CFD_TUNE_TENT_TH = 6        /* rows per band of the predictor's march (>= 4) */
+};
+int cfd_set_tuning(cfd_solver* s, int knob, int value);
 
 /* Timing collected with HIP events on the solver's stream. */
 int cfd_get_timing(cfd_solver* s, cfd_timing* out);

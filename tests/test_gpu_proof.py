@@ -8,10 +8,11 @@ bounds), and an iteration it cannot settle that way is evaluated exactly (the
 solve restarts, with the exact residual kernel, at the launch that computed
 it). The test must be invisible: the same iteration counts, the same reported
 residuals and the same fields, bit for bit, as exact residuals throughout
-(CFD_PROOF=0) and as the red-black oracle.
+(proof_test="off") and as the red-black oracle.
 """
 from __future__ import annotations
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -23,18 +24,13 @@ from test_gpu_parity import assert_bits  # noqa: E402
 FIELDS = ("p", "u", "v")
 
 
-@pytest.fixture(autouse=True)
-def multi_launch_path(monkeypatch):
-    monkeypatch.setenv("CFD_SMALL", "0")  # the multi-launch solve, at any size
-
-
 def run(monkeypatch, cp, steps, proof, ns=3, last_timing=False, **kw):
     """proof: the proof-mode test with `ns` sweeps per launch (3, or 4: no
     residual stage, so four sweeps fit the 8-row halos); else exact residuals.
+    Always the multi-launch solve (small_solve off), at any size.
     last_timing: timing of the last step only."""
-    monkeypatch.setenv("CFD_PROOF", "1" if proof else "0")
-    monkeypatch.setenv("CFD_PROOF_NS", str(ns))
-    g = C.CavitySolver(cp, device=0, **kw)
+    g = C.CavitySolver(cp, device=0, small_solve="off", proof_test="on" if proof else "off",
+                       sweeps_per_launch=ns if proof else 0, **kw)
     hist = []
     for s in range(steps):
         if last_timing and s == steps - 1:
@@ -122,3 +118,40 @@ def test_full_size_step_proven(monkeypatch, ns):
     pr = run(monkeypatch, cp, 2, True, ns, last_timing=True)
     same(ex, pr, f"4096^2, {ns} sweeps")
     assert pr[2].proof_fallbacks == 0
+
+
+def test_stop_in_first_proof_launch_after_fallback(monkeypatch):
+    """The first proof-mode launch after a fallback follows exact 3-sweep
+    launches and runs 4 sweeps: before the fix (kernels.hpp RING_AHEAD) its
+    4th ring slot was not cleared by the 3-sweep launch before it and kept an
+    old exact residual, which read as "proven to go on". With chunk 5 or 6 the
+    first step's fallback (iteration 1: the corner-only source moves no cell
+    that can prove) is followed by exact launches over iterations 1..15 (1..18)
+    and the first proof launch covers 16..19 (19..22). Tolerances are placed at
+    the exact residuals of iterations 10..30 so that the reference stops at
+    many iterations around that launch (SOR with omega 1.5 and the reference's
+    own): every solve must equal exact residuals throughout, bit for bit."""
+    stops = set()
+    for omega in (1.5, None):
+        kw = {"omega": omega} if omega else {}
+        r = {}
+        for k in range(10, 31):  # exact residual of iteration k = the reported residual of a solve capped at k
+            cp = C.make_params("cavity", nx=256, ny=256, max_iters=k, **kw)
+            (kk, res), = run(monkeypatch, cp, 1, False)[0]
+            assert kk == k
+            r[k] = res
+        g = C.CavitySolver(C.make_params("cavity", nx=256, ny=256, **kw), device=0, small_solve="off")
+        g.applyBoundaryConditions()
+        g.computeTentativeVelocities()
+        g.buildSourceTerm()
+        srcmax = float(np.abs(g.field("src")[1:-1, 1:-1]).max())
+        g.close()
+        for k in range(10, 31):
+            cp = C.make_params("cavity", nx=256, ny=256, **kw)
+            cp.tol_factor = r[k] / srcmax * (1.0 + 1e-9)
+            for chunk in (5, 6):
+                ex = run(monkeypatch, cp, 1, False, chunk=chunk)
+                pr = run(monkeypatch, cp, 1, True, 4, chunk=chunk)
+                same(ex, pr, f"omega {omega}, tolerance at iteration {k}, chunk {chunk}")
+                stops.add(ex[0][0][0])
+    assert len(stops) >= 3, stops

@@ -18,7 +18,7 @@ from cfd_amd import _lib  # noqa: E402
 from cfd_amd.dist import strip_rows  # noqa: E402
 
 
-def run_ranks(cp, world, steps, check_every=1, timing=False):
+def run_ranks(cp, world, steps, check_every=1, timing=False, **kw):
     L = _lib.lib()
     hub = L.cfd_comm_loopback_hub(world)
     assert hub
@@ -29,7 +29,7 @@ def run_ranks(cp, world, steps, check_every=1, timing=False):
         try:
             comm = L.cfd_comm_init_loopback(hub, r, 0)
             assert comm, L.cfd_last_error()
-            s = C.solver_for(cp, rank_rows=strip_rows(r, world, cp.ny), comm=comm, check_every=check_every)
+            s = C.solver_for(cp, rank_rows=strip_rows(r, world, cp.ny), comm=comm, check_every=check_every, **kw)
             if cp.case_id == C.CAVITY:
                 s.applyBoundaryConditions()
             its = [s.step() for _ in range(steps)]
@@ -52,8 +52,8 @@ def run_ranks(cp, world, steps, check_every=1, timing=False):
     return results
 
 
-def single(cp, steps):
-    s = C.solver_for(cp)
+def single(cp, steps, **kw):
+    s = C.solver_for(cp, **kw)
     if cp.case_id == C.CAVITY:
         s.applyBoundaryConditions()
     its = [s.step() for _ in range(steps)]
@@ -154,19 +154,16 @@ def test_overlapped_lagged_stop_and_caps(delta):
 
 
 @pytest.mark.parametrize("world,nx,ny,steps,cap", [(2, 256, 256, 3, 0), (3, 300, 240, 2, 0), (2, 512, 512, 2, 61)])
-def test_proof_mode_on_ranks(monkeypatch, world, nx, ny, steps, cap):
+def test_proof_mode_on_ranks(world, nx, ny, steps, cap):
     """The proof-mode convergence test on ranks: interior column
     tiles (nx >= 240), overlapped strips with the lagged test, ratios
     all-reduced (max) like residuals. Iteration counts and fields must equal
     one domain with exact residuals, bit for bit."""
     kw = {"max_iters": cap} if cap else {}
     cp = C.make_params("cavity", nx=nx, ny=ny, **kw)
-    monkeypatch.setenv("CFD_SMALL", "0")
-    monkeypatch.setenv("CFD_PROOF", "0")
-    s, its = single(cp, steps)
+    s, its = single(cp, steps, small_solve="off", proof_test="off")
     ref = s.field("p")
-    monkeypatch.setenv("CFD_PROOF", "1")
-    res = run_ranks(cp, world, steps)
+    res = run_ranks(cp, world, steps, proof_test="on")
     for r in res:
         assert r["overlapped"] > 0
         assert r["its"] == its

@@ -1,14 +1,12 @@
 """The one-workgroup LDS solve (small.hpp) used for reference-sized grids:
 whole timesteps bit-exact against the oracle's red-black restatement and
-against the multi-launch kernels (CFD_SMALL=0) on the reference's own grids
+against the multi-launch kernels (small_solve="off") on the reference's own grids
 (cavity 63², channel 93x31, step 256x32) and BASELINE configs[0] (128²) —
 the open cases against the oracle to 1e-8 (their source mean is re-associated)
 and bit-exact against the multi-launch path — the
 stop rule with check_every > 1, and the size limit (a grid just over it takes
 the multi-launch path with the same results)."""
 from __future__ import annotations
-
-import os
 
 import numpy as np
 import pytest
@@ -21,21 +19,13 @@ from test_gpu_parity import assert_bits, ofield  # noqa: E402
 
 
 def run_gpu(cp, steps, small=True, cavity=True, **kw):
-    old = os.environ.get("CFD_SMALL")
-    os.environ["CFD_SMALL"] = "1" if small else "0"
-    try:
-        g = C.solver_for(cp, **kw)
-        if cavity:  # cavity-01.cpp:380 (the open cases apply their BCs in the constructor)
-            g.applyBoundaryConditions()
-        its = [g.step() for _ in range(steps)]
-        fields = {n: g.field(n).copy() for n in ("u", "v", "p")}
-        tm = g.timing()
-        g.close()
-    finally:
-        if old is None:
-            del os.environ["CFD_SMALL"]
-        else:
-            os.environ["CFD_SMALL"] = old
+    g = C.solver_for(cp, small_solve="on" if small else "off", **kw)
+    if cavity:  # cavity-01.cpp:380 (the open cases apply their BCs in the constructor)
+        g.applyBoundaryConditions()
+    its = [g.step() for _ in range(steps)]
+    fields = {n: g.field(n).copy() for n in ("u", "v", "p")}
+    tm = g.timing()
+    g.close()
     return its, fields, tm
 
 

@@ -44,7 +44,35 @@ def test_nm_exports_match_header():
 
 
 def test_abi_version():
-    assert _lib.lib().cfd_abi_version() == 6
+    assert _lib.lib().cfd_abi_version() == 7
+
+
+def test_params_struct_layout_matches_header(tmp_path):
+    """The ctypes mirror of cfd_params has the C struct's size and field
+    offsets (ABI 7 appended proof_test / small_solve / overlap)."""
+    fields = [f for f, _ in _lib.CfdParams._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "cfd_amd.h"\nint main(void){\n'
+                   '  printf("%zu\\n", sizeof(cfd_params));\n'
+                   + "".join(f'  printf("%zu\\n", offsetof(cfd_params, {f}));\n' for f in fields)
+                   + '  printf("%d %d %d\\n", CFD_AUTO, CFD_ON, CFD_OFF);\n  return 0;\n}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    assert int(out[0]) == ctypes.sizeof(_lib.CfdParams)
+    for k, f in enumerate(fields):
+        assert int(out[1 + k]) == getattr(_lib.CfdParams, f).offset, f
+    assert out[1 + len(fields)].split() == [str(_lib.SWITCH[n]) for n in ("auto", "on", "off")]
+
+
+def test_switches_default_to_auto_and_map():
+    """cfd_params_init leaves the ABI-7 switches at CFD_AUTO; the Python
+    mirror passes "auto" / "on" / "off" through unchanged."""
+    lp = C.params_from_library(C.CAVITY)
+    assert (lp.proof_test, lp.small_solve, lp.overlap) == (0, 0, 0)
+    cp = C.solver.to_cparams(C.make_params("cavity"), proof_test="off", small_solve="on", overlap="off")
+    assert (cp.proof_test, cp.small_solve, cp.overlap) == (2, 1, 2)
+    assert set(_lib.TUNING.values()) == set(range(7))
 
 
 @pytest.mark.parametrize("case", ["cavity", "channel", "backwards_step"])
@@ -119,14 +147,28 @@ def test_invalid_params_rejected():
     assert b"unknown case" in _lib.lib().cfd_last_error()
 
 
-@pytest.mark.parametrize("case,spl,msg", [("channel", 3, b"cavity only"), ("cavity", 4, b"sweeps_per_launch"),
-                                          ("cavity", -1, b"sweeps_per_launch")])
-def test_sweeps_per_launch_validated_before_device(case, spl, msg):
+@pytest.mark.parametrize("case,spl,kw,msg", [
+    ("channel", 3, {}, b"cavity only"), ("channel", 4, {}, b"cavity only"),
+    ("cavity", 5, {}, b"sweeps_per_launch"), ("cavity", -1, {}, b"sweeps_per_launch"),
+    ("cavity", 4, {"proof_test": "off"}, b"proof-mode test"),
+    ("cavity", 4, {"ordering": "lex"}, b"lexicographic-order kernel"),
+])
+def test_sweeps_per_launch_validated_before_device(case, spl, kw, msg):
     """Parameter errors are reported before any device is touched (the checks
-    run first in the solver constructor), so they hold on CPU-only hosts too."""
+    run first in the solver constructor), so they hold on CPU-only hosts too.
+    Four sweeps per launch (the default proof-mode plan, stated) are accepted
+    for the red-black cavity with the proof test."""
     with pytest.raises(_lib.CfdError) as e:
-        C.solver_for(C.make_params(case), sweeps_per_launch=spl)
+        C.solver_for(C.make_params(case), sweeps_per_launch=spl, **kw)
     assert msg.decode() in str(e.value)
+
+
+def test_bad_switch_rejected_before_device():
+    cp = C.solver.to_cparams(C.make_params("cavity"))
+    cp.overlap = 7
+    h = _lib.lib().cfd_create(ctypes.byref(cp), 0, 1)
+    assert not h
+    assert b"cfd_switch" in _lib.lib().cfd_last_error()
 
 
 def test_no_cpu_fallback_without_gpu():
