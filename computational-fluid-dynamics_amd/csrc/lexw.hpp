@@ -171,15 +171,16 @@ __device__ __forceinline__ double2 lx_ld(const WaveCtx<CAVITY>& x, const double*
 // ran the ramp launches at half the steady kernel's speed.)
 constexpr int LX_ACT = 1;
 struct LxAct {
-  bool a, b, c;  // u, u-1, u-2 within [0, 2(K-1)]
+  bool a, b, c;    // u, u-1, u-2 within [0, 2(K-1)]
+  bool a2, b2;     // u-2, u-3: the same two half-sweeps later (open cases: the left / bottom ghosts)
 };
 template <int MODE>
 __device__ __forceinline__ LxAct lx_act(const LexCtx& lc, int gi, int R) {
-  if constexpr (!(MODE & LX_ACT)) return LxAct{true, true, true};
+  if constexpr (!(MODE & LX_ACT)) return LxAct{true, true, true, true, true};
   const unsigned span = 2u * (unsigned)(lc.K - 1);
   unsigned u = (unsigned)(lc.H0 - 1 - R - gi);
   asm volatile("" : "+v"(u));  // (opaque: no loop splitting on the induction variable R)
-  return LxAct{u <= span, u - 1u <= span, u - 2u <= span};
+  return LxAct{u <= span, u - 1u <= span, u - 2u <= span, u - 2u <= span, u - 3u <= span};
 }
 
 // SOR update (cavity-01.cpp:643-654) as pc*omm + om*sum in every cell. The
@@ -281,6 +282,102 @@ __device__ __forceinline__ void lx_row(const WaveCtx<CAVITY>& x, const LexCtx& l
   asm volatile("" : "+v"(exi));
 }
 
+// ---- open cases (channel) ----
+//
+// The reference's anisotropic update (channel-01.cpp:659-666, the divide
+// correctly rounded: kernels.hpp div_denom) in every interior cell. Its ghost
+// refresh after each sweep (applyPressureGhosts, channel-01.cpp:531-541: p[j][0]
+// = p[j][1], p[j][nx+1] = 0, p[0][i] = p[1][i], p[ny+1][i] = p[ny][i], corners
+// untouched) fits the skew as cells with a copy rule, updated in the half-sweep
+// of their colour:
+//  * a ghost AFTER its interior neighbour in the reference's order (top row
+//    ny+1, right column nx+1) takes its k-th value at its own skew time
+//    i+j+2(k-1), one half-sweep after the neighbour's iteration k: the copy
+//    (or 0) the neighbour reads in iteration k+1 as p_prev;
+//  * a ghost BEFORE it (left column 0, bottom row 0) is read by the neighbour as
+//    p_new, refreshed by the previous sweep, so it copies the neighbour's
+//    iteration k-1 value at i+j+2(k-1) for k = 2 .. K+1: two half-sweeps later
+//    than a cell of its position (the reference's first sweep reads the stored
+//    ghost; the last copy is the refresh after sweep K).
+// Residuals (channel-01.cpp:672-681) see the ghosts refreshed after the sweep:
+// a top / right ghost is updated in the half-sweep the residual is evaluated
+// in (its new value is at hand); a left / bottom one is not yet, so the
+// interior cell's own value stands in for it (the copy it will take).
+// Interior bands whose march stays off the ghost rows and the halo edges take
+// the unmasked update (RC = false); the others choose per row (row-uniform).
+struct LxoCol {
+  int ka, kb;  // per slot: 0 keep (outside the grid), 1 left ghost, 2 right ghost, 3 interior
+};
+__device__ __forceinline__ int lxo_kind(const WaveCtx<CAVITY>& x, int i) {
+  return (i < 0 || i > x.g.nx + 1) ? 0 : (i == 0) ? 1 : (i == x.g.nx + 1) ? 2 : 3;
+}
+
+template <int CASE, bool EDGE, bool RC>
+__device__ __forceinline__ double lxo_value(const WaveCtx<CAVITY>& x, int rk, int ck, double pc, double pW, double pE,
+                                            double pS, double pN, double fc) {
+  const double sor = sor_update<CASE>(x.c, 0, 0, 0, 0, pc, pW, pE, pS, pN, fc);
+  if constexpr (!RC && !EDGE) return sor;
+  double nv = sor;
+  if constexpr (EDGE) nv = (ck == 3) ? sor : (ck == 1) ? pE : (ck == 2) ? 0.0 : pc;
+  if constexpr (RC) {  // row kinds: 1 bottom ghost (copy N), 2 top ghost (copy S), 3 keep
+    const double g = (rk == 1) ? pN : pS;
+    if (EDGE) nv = (rk == 0) ? nv : (rk != 3 && ck == 3) ? g : pc;
+    else nv = (rk == 0) ? nv : (rk != 3) ? g : pc;
+  }
+  return nv;
+}
+
+template <int CASE, int ROT, int JPAR, int COLOR, int MODE, bool EDGE, bool RC, bool STORE, bool RES>
+__device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxoCol& cc,
+                                        double2 (&W)[5], int j, int X, const LxAct& act, const double2& fc, int& exi) {
+  double2& m = W[LX_SLOT(X)];
+  const double2 nb = W[LX_SLOT(X + 1)], sb = W[LX_SLOT(X - 1)];  // rows j+1 (N), j-1 (S)
+  const double2 old = m;
+  // row kind (row-uniform): 0 interior, 1 bottom ghost, 2 top ghost, 3 keep (halo edge / outside)
+  const int rk = !RC ? 0 : (j == 0) ? 1 : (j == x.g.ny + 1) ? 2 : (j > x.rmin && j < x.rmax) ? 0 : 3;
+  constexpr bool A = ((JPAR ^ COLOR) & 1) == 0;
+  if constexpr (A) {
+    const double nv = lxo_value<CASE, EDGE, RC>(x, rk, cc.ka, m.x, dpp_from_left(m.y), m.y, sb.x, nb.x, fc.x);
+    if constexpr ((MODE & LX_ACT) != 0) {
+      const bool shifted = (RC && rk == 1) || (EDGE && cc.ka == 1);  // left / bottom ghost: two half-sweeps later
+      m.x = (shifted ? act.a2 : act.a) ? nv : m.x;
+    } else {
+      m.x = nv;
+    }
+  } else {  // (column 0 is always slot a)
+    const double nv = lxo_value<CASE, EDGE, RC>(x, rk, cc.kb, m.y, m.x, dpp_from_right(m.x), sb.y, nb.y, fc.y);
+    if constexpr ((MODE & LX_ACT) != 0) m.y = ((RC && rk == 1) ? act.b2 : act.b) ? nv : m.y;
+    else m.y = nv;
+  }
+  if (STORE && j >= x.y0 && j < x.y1 && x.out_lane) {
+    double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    d2v mv = {m.x, m.y};
+    __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
+  }
+  if constexpr (!RES) return;
+  const bool rrow = j >= x.y0 && j < x.y1 && j >= x.g.j0 && j <= x.g.j1;  // row-uniform
+  const double thr = rrow ? lc.tol : __builtin_huge_val();
+  const bool row1 = RC && j == 1;  // S is the bottom ghost: the cell's own value stands in
+  bool ex;
+  if constexpr (A) {  // the other colour at gi+1: W = gi (old; the left ghost when gi+1 == 1), E = gi+2 (new)
+    const double pc = m.y;
+    const double pW = (EDGE && x.gi == 0) ? pc : old.x;
+    const double pS = row1 ? pc : sb.y;
+    ex = fabs(residual_at<CASE>(x.c, 0, 0, 0, 0, pc, pW, dpp_from_right(m.x), pS, nb.y, fc.y)) > thr;
+    if constexpr (EDGE) ex = ex && cc.kb == 3;
+    if constexpr ((MODE & LX_ACT) != 0) ex = ex && act.c;
+  } else {  // the other colour at gi: W = gi-1 (old; gi is even, never column 1), E = gi+1 (new)
+    const double pc = m.x;
+    const double pS = row1 ? pc : sb.x;
+    ex = fabs(residual_at<CASE>(x.c, 0, 0, 0, 0, pc, dpp_from_left(old.y), m.y, pS, nb.x, fc.x)) > thr;
+    if constexpr (EDGE) ex = ex && cc.ka == 3;
+    if constexpr ((MODE & LX_ACT) != 0) ex = ex && act.b;
+  }
+  exi = ex ? 1 : exi;
+  asm volatile("" : "+v"(exi));
+}
+
 // Sampled residuals (MODE & LX_SAMPLE): the loop goes on iff SOME cell's
 // residual exceeds tol, so the exact residual of a subset of the cells proves
 // "go on" whenever one of them exceeds it. A sampled march evaluates the rows
@@ -293,22 +390,36 @@ constexpr int LX_SAMPLE = 2;
 template <int MODE, int T, int X>
 constexpr bool lx_res_row() { return !(MODE & LX_SAMPLE) || T == X; }
 
-template <int S, int NS, int T, int ROT, int PAR, int MODE, bool EDGE>
-__device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCol (&cc)[2],
+// column data of a wave: the cavity's wall kinds (LxCol) / the open cases' ghost kinds (LxoCol)
+template <int CASE>
+struct LxCols {
+  LxCol cc[2];
+  LxoCol oc;
+};
+
+template <int CASE, int S, int NS, int T, int ROT, int PAR, int MODE, bool EDGE, bool RC>
+__device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCols<CASE>& cl,
                                           LexRun<NS>& s, int R, const LxAct& act, int& exi) {
   if constexpr (S < NS) {
     // red at R+2S+1 (parity PAR^1) in half-sweep H0+2S; black at R+2S+2 (PAR) in H0+2S+1
-    lx_row<ROT, PAR ^ 1, 0, MODE, EDGE, false, lx_res_row<MODE, T, 2 * S + 1>()>(
-        x, lc, cc, s.w[S], R + 2 * S + 1, 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi);
-    lx_row<ROT, PAR, 1, MODE, EDGE, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>()>(
-        x, lc, cc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi);
+    if constexpr (CASE == CAVITY) {
+      lx_row<ROT, PAR ^ 1, 0, MODE, EDGE, false, lx_res_row<MODE, T, 2 * S + 1>()>(
+          x, lc, cl.cc, s.w[S], R + 2 * S + 1, 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi);
+      lx_row<ROT, PAR, 1, MODE, EDGE, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>()>(
+          x, lc, cl.cc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi);
+    } else {
+      lxo_row<CASE, ROT, PAR ^ 1, 0, MODE, EDGE, RC, false, lx_res_row<MODE, T, 2 * S + 1>()>(
+          x, lc, cl.oc, s.w[S], R + 2 * S + 1, 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi);
+      lxo_row<CASE, ROT, PAR, 1, MODE, EDGE, RC, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>()>(
+          x, lc, cl.oc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi);
+    }
     if constexpr (S + 1 < NS) s.w[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
-    lx_sweeps<S + 1, NS, T, ROT, PAR, MODE, EDGE>(x, lc, cc, s, R, act, exi);
+    lx_sweeps<CASE, S + 1, NS, T, ROT, PAR, MODE, EDGE, RC>(x, lc, cl, s, R, act, exi);
   }
 }
 
-template <int NS, int T, int ROT, int PAR, int MODE, bool EDGE>  // PAR = parity of R, T = step of the unroll
-__device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCol (&cc)[2],
+template <int CASE, int NS, int T, int ROT, int PAR, int MODE, bool EDGE, bool RC>  // PAR = parity of R, T = step of the unroll
+__device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCols<CASE>& cl,
                                         LexRun<NS>& s, int R, unsigned long long bit) {
   s.w[0][LX_SLOT(0)] = s.np[LX_SLOT(0)];
   s.fr[LX_S10(1)] = s.nf[LX_SLOT(0)];
@@ -316,7 +427,7 @@ __device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& 
   s.nf[LX_SLOT(-4)] = lx_ld(x, x.f, R - 3);
   int exi = 0;
   const LxAct act = lx_act<MODE>(lc, x.gi, R);
-  lx_sweeps<0, NS, T, ROT, PAR, MODE, EDGE>(x, lc, cc, s, R, act, exi);
+  lx_sweeps<CASE, 0, NS, T, ROT, PAR, MODE, EDGE, RC>(x, lc, cl, s, R, act, exi);
   if constexpr ((MODE & LX_SAMPLE) && (T < 1 || T > 2 * NS)) return;  // (no residual row at this step)
   s.mask |= exi ? bit : 0ull;
 }
@@ -345,7 +456,7 @@ __device__ __forceinline__ void lexw_flush(const LexCtl& L, int sh, int q0, cons
   }
 }
 
-template <int NS, int MODE, bool EDGE>
+template <int CASE, int NS, int MODE, bool EDGE, bool RC = false>
 __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L, int y0, int y1,
                                          int c0, int lane, int shard) {
   constexpr int H = 2 * NS + 1;
@@ -369,22 +480,23 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
     }
   }
   s.mask = 0ull;
-  LxCol cc[2];
-  if constexpr (EDGE) cc[0] = lx_col(x, x.gi), cc[1] = lx_col(x, x.gi + 1);
+  LxCols<CASE> cl;
+  if constexpr (EDGE && CASE == CAVITY) cl.cc[0] = lx_col(x, x.gi), cl.cc[1] = lx_col(x, x.gi + 1);
+  if constexpr (EDGE && CASE != CAVITY) cl.oc = LxoCol{lxo_kind(x, x.gi), lxo_kind(x, x.gi + 1)};
   int R = Rbeg;
   // (nsteps + 9 <= 127 by the host's band limit: bits t/2 < 64)
 #define LX_BIT(T) ((((st + (T)) >> 1) < 64) ? (1ull << ((st + (T)) >> 1)) : 0ull)
   for (int st = 0; st < nsteps; st += 10, R -= 10) {
-    lx_step<NS, 0, 0, 0, MODE, EDGE>(x, lc, cc, s, R, LX_BIT(0));
-    lx_step<NS, 1, 1, 1, MODE, EDGE>(x, lc, cc, s, R - 1, LX_BIT(1));
-    lx_step<NS, 2, 2, 0, MODE, EDGE>(x, lc, cc, s, R - 2, LX_BIT(2));
-    lx_step<NS, 3, 3, 1, MODE, EDGE>(x, lc, cc, s, R - 3, LX_BIT(3));
-    lx_step<NS, 4, 4, 0, MODE, EDGE>(x, lc, cc, s, R - 4, LX_BIT(4));
-    lx_step<NS, 5, 0, 1, MODE, EDGE>(x, lc, cc, s, R - 5, LX_BIT(5));
-    lx_step<NS, 6, 1, 0, MODE, EDGE>(x, lc, cc, s, R - 6, LX_BIT(6));
-    lx_step<NS, 7, 2, 1, MODE, EDGE>(x, lc, cc, s, R - 7, LX_BIT(7));
-    lx_step<NS, 8, 3, 0, MODE, EDGE>(x, lc, cc, s, R - 8, LX_BIT(8));
-    lx_step<NS, 9, 4, 1, MODE, EDGE>(x, lc, cc, s, R - 9, LX_BIT(9));
+    lx_step<CASE, NS, 0, 0, 0, MODE, EDGE, RC>(x, lc, cl, s, R, LX_BIT(0));
+    lx_step<CASE, NS, 1, 1, 1, MODE, EDGE, RC>(x, lc, cl, s, R - 1, LX_BIT(1));
+    lx_step<CASE, NS, 2, 2, 0, MODE, EDGE, RC>(x, lc, cl, s, R - 2, LX_BIT(2));
+    lx_step<CASE, NS, 3, 3, 1, MODE, EDGE, RC>(x, lc, cl, s, R - 3, LX_BIT(3));
+    lx_step<CASE, NS, 4, 4, 0, MODE, EDGE, RC>(x, lc, cl, s, R - 4, LX_BIT(4));
+    lx_step<CASE, NS, 5, 0, 1, MODE, EDGE, RC>(x, lc, cl, s, R - 5, LX_BIT(5));
+    lx_step<CASE, NS, 6, 1, 0, MODE, EDGE, RC>(x, lc, cl, s, R - 6, LX_BIT(6));
+    lx_step<CASE, NS, 7, 2, 1, MODE, EDGE, RC>(x, lc, cl, s, R - 7, LX_BIT(7));
+    lx_step<CASE, NS, 8, 3, 0, MODE, EDGE, RC>(x, lc, cl, s, R - 8, LX_BIT(8));
+    lx_step<CASE, NS, 9, 4, 1, MODE, EDGE, RC>(x, lc, cl, s, R - 9, LX_BIT(9));
   }
 #undef LX_BIT
   // lane l's bit u <-> iteration Bd0 + u - l = (Bd0 - 63) + (u + 63 - l):
@@ -403,10 +515,19 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
 // H0-1), or finished in the previous launch and must be copied into this
 // launch's output buffer (i+j+2(K-1) >= H0-2NS). Other rows hold their final
 // values in both buffers already.
-__host__ __device__ inline void lexw_rows(const Geo& g, int H0, int K, int ns, int ct, int* lo, int* hi) {
-  const int cmin = max(ct * PAIR_TWC, 1), cmax = min(ct * PAIR_TWC + PAIR_TWC - 1, g.nx);
-  *lo = max(g.j0, H0 - 2 * ns - 2 * (K - 1) - cmax);
-  *hi = min(g.j1, H0 + 2 * ns - 1 - cmin);
+// Open cases: the ghost rows / columns too, the left / bottom ghosts active two
+// half-sweeps later than their position (lxo_row).
+__host__ __device__ inline void lexw_rows(const Geo& g, int H0, int K, int ns, int ct, int* lo, int* hi,
+                                          bool open = false) {
+  if (!open) {
+    const int cmin = max(ct * PAIR_TWC, 1), cmax = min(ct * PAIR_TWC + PAIR_TWC - 1, g.nx);
+    *lo = max(g.j0, H0 - 2 * ns - 2 * (K - 1) - cmax);
+    *hi = min(g.j1, H0 + 2 * ns - 1 - cmin);
+  } else {
+    const int cmin = max(ct * PAIR_TWC, 0), cmax = min(ct * PAIR_TWC + PAIR_TWC - 1, g.nx + 1);
+    *lo = max(g.wj0, H0 - 2 * ns - 2 * (K - 1) - cmax - 2);
+    *hi = min(g.wj1, H0 + 2 * ns - 1 - cmin);
+  }
 }
 
 // One launch of NS lexicographic-order sweeps (half-sweeps H0 .. H0+2NS-1) on
@@ -415,11 +536,13 @@ __host__ __device__ inline void lexw_rows(const Geo& g, int H0, int K, int ns, i
 // waves per SIMD); RAMP = true: the launches at the start and the end of the
 // solve, whose tiles take the masked marches unless wholly active (the masked
 // code would cost the steady kernel registers, so it lives in its own kernel).
-template <int NS, bool RAMP, bool SAMPLE = false>
+template <int CASE, int NS, bool RAMP, bool SAMPLE = false>
 __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisson_lexw_kernel(Geo g, Coef c, const double* __restrict__ pin,
                                                               double* __restrict__ pout, const double* __restrict__ f,
                                                               LexCtl L, int H0, int K, int ka, int kb, PairPlan pl,
                                                               int flags, LexRamp rp) {
+  static_assert(CASE == CAVITY || CASE == CHANNEL, "reference-order march: cavity and channel");
+  constexpr bool OPEN = CASE != CAVITY;
   constexpr int CH = 8;  // column halo (lanes 0-3 and 60-63)
   constexpr int H = 2 * NS + 1;
   const int lane = threadIdx.x & 63;
@@ -444,7 +567,7 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     ctile = ca + (tile - (int)(e >> 16));
     if (ctile > cb) return;
     int rlo, rhi;
-    lexw_rows(g, H0, K, NS, ctile, &rlo, &rhi);
+    lexw_rows(g, H0, K, NS, ctile, &rlo, &rhi, OPEN);
     y0 = max(rp.row0 + lo * rp.th, rlo);
     y1 = min(rp.row0 + (lo + 1) * rp.th, rhi + 1);
   } else {
@@ -474,16 +597,19 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   if (y0 >= y1) return;
 
   // activity of the marched region (rows y0-H-1 .. y1+H, columns c0 .. c0+127,
-  // interior cells) over this launch's half-sweeps (and the previous launch's
-  // last one, whose black residuals this launch evaluates)
-  const int rlo = max(max(y0 - H - 1, 1), g.row_lo), rhi = min(min(y1 + H, g.ny), g.row_lo + g.nrows - 1);
-  const int clo = max(c0, 1), chi = min(c0 + 127, g.nx);
+  // interior cells; open cases: ghosts too, the left / bottom ones two
+  // half-sweeps late) over this launch's half-sweeps (and the previous
+  // launch's last one, whose black residuals this launch evaluates)
+  constexpr int GLO = OPEN ? 0 : 1;  // lowest row / column index with cells that change
+  const int rlo = max(max(y0 - H - 1, GLO), g.row_lo);
+  const int rhi = min(min(y1 + H, g.ny + 1 - GLO), g.row_lo + g.nrows - 1);
+  const int clo = max(c0, GLO), chi = min(c0 + 127, g.nx + 1 - GLO);
   const int smin = clo + rlo, smax = chi + rhi;
   const int Hend = H0 + 2 * NS - 1;
-  const int last = 2 * (K - 1);
+  const int last = 2 * (K - 1) + (OPEN ? 2 : 0);
   if (smin > Hend) return;                // not started: both buffers hold the initial field
   if (smax + last < H0 - 2 * NS) return;  // finished before the previous launch: both hold the result
-  const bool cols_in = clo == c0 && chi == c0 + 127;
+  const bool cols_in = OPEN ? (c0 >= 1 && c0 + 127 <= g.nx) : (clo == c0 && chi == c0 + 127);
 
   WaveCtx<CAVITY> x{g, c};
   x.pin = pin; x.pout = pout; x.f = f;
@@ -508,16 +634,33 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   const int shard = bl & (LEXW_SHARDS - 1);
   const bool edge = !cols_in;
   constexpr int SM = SAMPLE ? LX_SAMPLE : 0;
-  if constexpr (RAMP) {
-    // tiles of a ramp launch whose every cell is active in every half-sweep
-    // it evaluates (H0-1 .. H0+2NS-1) take the unmasked march
-    const bool full = smax <= H0 - 2 && Hend <= smin + last;
-    if (edge) lx_march<NS, LX_ACT | SM, true>(x, lc, L, y0, y1, c0, lane, shard);
-    else if (full) lx_march<NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard);
-    else lx_march<NS, LX_ACT | SM, false>(x, lc, L, y0, y1, c0, lane, shard);
+  if constexpr (!OPEN) {
+    if constexpr (RAMP) {
+      // tiles of a ramp launch whose every cell is active in every half-sweep
+      // it evaluates (H0-1 .. H0+2NS-1) take the unmasked march
+      const bool full = smax <= H0 - 2 && Hend <= smin + last;
+      if (edge) lx_march<CASE, NS, LX_ACT | SM, true>(x, lc, L, y0, y1, c0, lane, shard);
+      else if (full) lx_march<CASE, NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard);
+      else lx_march<CASE, NS, LX_ACT | SM, false>(x, lc, L, y0, y1, c0, lane, shard);
+    } else {
+      if (edge) lx_march<CASE, NS, SM, true>(x, lc, L, y0, y1, c0, lane, shard);
+      else lx_march<CASE, NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard);
+    }
   } else {
-    if (edge) lx_march<NS, SM, true>(x, lc, L, y0, y1, c0, lane, shard);
-    else lx_march<NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard);
+    // row checks unless every row the march updates (y0-H+1 .. y1+H+2NS) lies
+    // strictly between the stored strip's edge rows (ghost rows included)
+    const bool rc = !(y0 - H + 1 > x.rmin && y1 + H + 2 * NS < x.rmax);
+    if constexpr (RAMP) {
+      const bool full = !rc && smax <= H0 - 2 && Hend <= smin + 2 * (K - 1);
+      if (edge) lx_march<CASE, NS, LX_ACT | SM, true, true>(x, lc, L, y0, y1, c0, lane, shard);
+      else if (full) lx_march<CASE, NS, SM, false, false>(x, lc, L, y0, y1, c0, lane, shard);
+      else if (rc) lx_march<CASE, NS, LX_ACT | SM, false, true>(x, lc, L, y0, y1, c0, lane, shard);
+      else lx_march<CASE, NS, LX_ACT | SM, false, false>(x, lc, L, y0, y1, c0, lane, shard);
+    } else {
+      if (edge) lx_march<CASE, NS, SM, true, true>(x, lc, L, y0, y1, c0, lane, shard);
+      else if (rc) lx_march<CASE, NS, SM, false, true>(x, lc, L, y0, y1, c0, lane, shard);
+      else lx_march<CASE, NS, SM, false, false>(x, lc, L, y0, y1, c0, lane, shard);
+    }
   }
 }
 
@@ -547,6 +690,24 @@ __global__ __launch_bounds__(256) void cavity_resmax_kernel(Geo g, Coef c, const
     const double ra = residual_abs<CAVITY>(c, nx, ny, j, gi, pc.x, pw, pc.y, ps.x, pn.x, fc.x);
     const double rb = residual_abs<CAVITY>(c, nx, ny, j, gi + 1, pc.y, pc.x, pe, ps.y, pn.y, fc.y);
     m = fmax(gi >= 1 ? ra : 0.0, gi + 1 <= nx ? rb : 0.0);
+  }
+  block_max_to_shard<256>(m, shards, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
+}
+
+// max-norm residual of an open-case field over its fluid cells
+// (channel-01.cpp:672-681, backwards_step-01.cpp:916-930), ghosts as stored
+// (the final field's are refreshed): the residual the reference reports after
+// its last sweep, in lexicographic mode. One cell per thread.
+template <int CASE>
+__global__ __launch_bounds__(256) void open_resmax_kernel(Geo g, Coef c, const double* __restrict__ p,
+                                                          const double* __restrict__ f, double* __restrict__ shards) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63) + 1;
+  const int j = max(g.j0, 1) + blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int nx = g.nx, ny = g.ny;
+  double m = 0.0;
+  if (j <= min(g.j1, ny) && i <= nx && is_fluid(c, nx, ny, j, i)) {
+    const size_t o = at(g, j, i), P = (size_t)g.pitch;
+    m = residual_abs<CASE>(c, nx, ny, j, i, p[o], p[o - 1], p[o + 1], p[o - P], p[o + P], f[o]);
   }
   block_max_to_shard<256>(m, shards, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
 }

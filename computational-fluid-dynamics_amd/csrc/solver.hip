@@ -191,8 +191,15 @@ class Solver {
   hipEvent_t ev_f0 = nullptr, ev_f1 = nullptr;
   int resident_lexw_waves = 2048;
   int lexw_edge_pct = 100;  // wall-tile bands as long as interior ones (measured at 4096^2; CFD_LEXW_EDGE_PCT)
-  bool use_lexw() const { return P.ordering == CFD_ORDER_LEX && P.case_id == CFD_CAVITY; }
-  int lexw_ns() const { return P.sweeps_per_launch >= 1 ? P.sweeps_per_launch : 3; }
+  // the multi-block reference-order march (lexw.hpp): cavity (1-3 sweeps per
+  // launch) and channel (3); the backwards step keeps the one-workgroup kernel
+  bool use_lexw() const {
+    return P.ordering == CFD_ORDER_LEX && (P.case_id == CFD_CAVITY || P.case_id == CFD_CHANNEL);
+  }
+  int lexw_ns() const {
+    if (P.case_id != CFD_CAVITY) return 3;
+    return P.sweeps_per_launch >= 1 ? P.sweeps_per_launch : 3;
+  }
 
   // Rayleigh-Benard: the cavity's projection (P.case_id is set to CFD_CAVITY,
   // u_ref 0 = lid at rest) plus the temperature stage on tcur/tnext.
@@ -252,9 +259,14 @@ class Solver {
       }
       if (use_lexw()) {
         int lps = 0;
-        if (lexw_ns() == 1) HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<1, false>, 256, 0));
-        else if (lexw_ns() == 2) HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<2, false>, 256, 0));
-        else HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<3, false, true>, 256, 0));
+        if (P.case_id == CFD_CHANNEL)
+          HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<CHANNEL, 3, false, true>, 256, 0));
+        else if (lexw_ns() == 1)
+          HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<CAVITY, 1, false>, 256, 0));
+        else if (lexw_ns() == 2)
+          HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<CAVITY, 2, false>, 256, 0));
+        else
+          HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<CAVITY, 3, false, true>, 256, 0));
         resident_lexw_waves = std::max(1, std::min(lps, 4)) * 4 * prop.multiProcessorCount;
       }
       resident_pair_waves = pps * 4 * prop.multiProcessorCount;
@@ -431,8 +443,8 @@ class Solver {
       throw Error(CFD_E_ARG, "lexicographic ordering runs on one device (strips allowed), not on ranks");
     // (the cavity's lexicographic solve runs on the multi-block wavefront kernel
     // at any size; the open cases on the one-workgroup kernel)
-    if (P.ordering == CFD_ORDER_LEX && P.case_id != CFD_CAVITY && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
-      throw Error(CFD_E_ARG, "lexicographic ordering of the open cases supports nx + ny < 12000");
+    if (P.ordering == CFD_ORDER_LEX && P.case_id == CFD_BACKSTEP && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
+      throw Error(CFD_E_ARG, "lexicographic ordering of the backwards step supports nx + ny < 12000");
     if (P.case_id == CFD_BACKSTEP && (P.step_i <= 0 || P.step_i >= P.nx))
       throw Error(CFD_E_ARG, "Step location is outside computational domain!");
     if (P.case_id == CFD_BACKSTEP && (P.inlet_jmax < 1 || P.inlet_jmax > P.ny))
@@ -540,8 +552,9 @@ class Solver {
       check_launch("source");
     }
     if (P.case_id != CFD_CAVITY) {
-      if (P.ordering == CFD_ORDER_LEX) {  // the reference's sequential sum, bit for bit
-        seq_sum_kernel<<<1, 64, 0, st>>>(S[0].g, C, S[0].b[B_F], nullptr, 0, total);
+      if (P.ordering == CFD_ORDER_LEX) {  // the reference's sequential sum, bit for bit (strips in order)
+        for (size_t q = 0; q < S.size(); ++q)
+          seq_sum_kernel<<<1, 64, 0, st>>>(S[q].g, C, S[q].b[B_F], nullptr, 0, total, q > 0);
       } else {
         sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total);
       }
@@ -860,7 +873,7 @@ class Solver {
       long long tot = 0;
       std::vector<std::pair<int, int>> rr(pl.ctiles);
       for (int c = 0; c < pl.ctiles; ++c) {
-        lexw_rows(g, H0, K, ns, c, &rr[c].first, &rr[c].second);
+        lexw_rows(g, H0, K, ns, c, &rr[c].first, &rr[c].second, P.case_id != CFD_CAVITY);
         if (rr[c].second >= rr[c].first) {
           rl = std::min(rl, rr[c].first);
           rh = std::max(rh, rr[c].second);
@@ -899,13 +912,16 @@ class Solver {
     }
     if (ntiles == 0) return;
     const dim3 grid((ntiles + 3) / 4);
-#define CFD_LEXW_LAUNCH(NS, R, SM) \
-  poisson_lexw_kernel<NS, R, SM><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl, rp)
-    // (sampled residual rows: the 3-sweep kernel, the default; 1 and 2 sweeps evaluate every row)
-    if (ns == 1) { if (steady) CFD_LEXW_LAUNCH(1, false, false); else CFD_LEXW_LAUNCH(1, true, false); }
-    else if (ns == 2) { if (steady) CFD_LEXW_LAUNCH(2, false, false); else CFD_LEXW_LAUNCH(2, true, false); }
-    else if (sample) { if (steady) CFD_LEXW_LAUNCH(3, false, true); else CFD_LEXW_LAUNCH(3, true, true); }
-    else { if (steady) CFD_LEXW_LAUNCH(3, false, false); else CFD_LEXW_LAUNCH(3, true, false); }
+#define CFD_LEXW_LAUNCH(CASE, NS, R, SM) \
+  poisson_lexw_kernel<CASE, NS, R, SM><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl, rp)
+    // (sampled residual rows: the 3-sweep kernels, the default; 1 and 2 sweeps evaluate every row)
+    if (P.case_id == CFD_CHANNEL) {
+      if (sample) { if (steady) CFD_LEXW_LAUNCH(CHANNEL, 3, false, true); else CFD_LEXW_LAUNCH(CHANNEL, 3, true, true); }
+      else { if (steady) CFD_LEXW_LAUNCH(CHANNEL, 3, false, false); else CFD_LEXW_LAUNCH(CHANNEL, 3, true, false); }
+    } else if (ns == 1) { if (steady) CFD_LEXW_LAUNCH(CAVITY, 1, false, false); else CFD_LEXW_LAUNCH(CAVITY, 1, true, false); }
+    else if (ns == 2) { if (steady) CFD_LEXW_LAUNCH(CAVITY, 2, false, false); else CFD_LEXW_LAUNCH(CAVITY, 2, true, false); }
+    else if (sample) { if (steady) CFD_LEXW_LAUNCH(CAVITY, 3, false, true); else CFD_LEXW_LAUNCH(CAVITY, 3, true, true); }
+    else { if (steady) CFD_LEXW_LAUNCH(CAVITY, 3, false, false); else CFD_LEXW_LAUNCH(CAVITY, 3, true, false); }
 #undef CFD_LEXW_LAUNCH
   }
 
@@ -920,7 +936,9 @@ class Solver {
   // sampled cell exceeds the tolerance).
   int run_lexw(int base, int K, bool tests, int kexact, int ka0, int* kstop, int* code, bool time_steady) {
     const int ns = lexw_ns();
-    const int Hlast = P.nx + P.ny + 2 * (K - 1);
+    // the last half-sweep: cell (ny, nx)'s K-th update, and for the open cases
+    // the top ghost (ny+1, nx)'s K-th copy one half-sweep later (lxo_row)
+    const int Hlast = P.nx + P.ny + 2 * (K - 1) + (P.case_id != CFD_CAVITY ? 1 : 0);
     const int nl = (Hlast - 2) / (2 * ns) + 1;  // last launch covers Hlast
     const int kmax = lexw_offset();
     LexCtl L{lexbits, (int)(lexbits_words / LEXW_SHARDS), kmax, tolv, stop, kexact};
@@ -1022,8 +1040,11 @@ class Solver {
   // reference's iteration k + q).
   int lex_hint = 0;  // the previous lexicographic solve's iteration count if it converged, else 0
 
-  // p buffers of every strip := `b`'s contents (fill) or zero (b < 0)
+  // p buffers of every strip := buffer `src_buf`'s contents, or the solve's
+  // initial field (src_buf < 0): zero for the cavity (cavity-01.cpp:610-611),
+  // the previous pressure for the open cases (channel-01.cpp:636, kept in B_PL)
   void lex_set_both(int src_buf) {
+    if (src_buf < 0 && P.case_id != CFD_CAVITY) src_buf = B_PL;
     for (auto& s : S) {
       const size_t bytes = (size_t)s.g.nrows * pitch * sizeof(double);
       for (int b : {0, 1}) {
@@ -1052,8 +1073,13 @@ class Solver {
     const int ns = lexw_ns();
     const int K = P.max_iters;
     const int base = pcur & 1;
-    // cavity-01.cpp:610-611: each solve starts from a zero field (both buffers:
-    // cells not yet started are read from either)
+    // the initial field in both buffers (cells not yet started are read from
+    // either): zero for the cavity (cavity-01.cpp:610-611); the open cases start
+    // from the previous pressure (channel-01.cpp:636), saved in B_PL for replays
+    if (P.case_id != CFD_CAVITY)
+      for (auto& s : S)
+        HIPC(hipMemcpyAsync(s.b[B_PL], s.b[pbuf(base)], (size_t)s.g.nrows * pitch * sizeof(double),
+                            hipMemcpyDeviceToDevice, st));
     lex_set_both(-1);
     solve_tolerance();
     if (multi()) exchange(B_F, HALO - 1);
@@ -1095,9 +1121,9 @@ class Solver {
         iters = kstop;
         fin = b1;
         res = rk;
-      } else {  // continuation from iteration kstop's field, every cell evaluated
+      } else {  // continuation from iteration kstop's field (kept in B_P2), every cell evaluated
         for (auto& s : S)
-          HIPC(hipMemcpyAsync(s.b[B_PL], s.b[pbuf(b1)], (size_t)s.g.nrows * pitch * sizeof(double),
+          HIPC(hipMemcpyAsync(s.b[B_P2], s.b[pbuf(b1)], (size_t)s.g.nrows * pitch * sizeof(double),
                               hipMemcpyDeviceToDevice, st));
         lex_set_both(pbuf(b1));
         lex_reset_tests();
@@ -1107,7 +1133,7 @@ class Solver {
         T.poisson_sweeps += (long long)n3 * ns;
         if (code2 == 1) {  // stops at kstop + k2 (< K): redo k2 iterations from kstop's field
           iters = kstop + k2;
-          lex_set_both(B_PL);
+          lex_set_both(B_P2);
           fin = lex_replay(b1, k2);
         } else {
           iters = K;
@@ -1197,8 +1223,15 @@ class Solver {
     if (multi()) exchange(bp, 1);
     HIPC(hipMemsetAsync(resmax, 0, RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
     for (auto& s : S) {
-      cavity_resmax_kernel<<<pair_grid(s), 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_F], resmax);
-      check_launch("cavity_resmax");
+      if (P.case_id == CFD_CAVITY) {
+        cavity_resmax_kernel<<<pair_grid(s), 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_F], resmax);
+      } else {
+        const int rows = std::min(s.g.j1, P.ny) - std::max(s.g.j0, 1) + 1;
+        const dim3 grid((P.nx + 63) / 64, std::max(1, (rows + 3) / 4));
+        if (P.case_id == CFD_CHANNEL) open_resmax_kernel<CHANNEL><<<grid, 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_F], resmax);
+        else open_resmax_kernel<BACKSTEP><<<grid, 256, 0, st>>>(s.g, C, s.b[bp], s.b[B_F], resmax);
+      }
+      check_launch("resmax");
     }
     if (comm && comm->nranks > 1) comm_allreduce_max(comm, resmax, RES_SHARDS * SHARD_STRIDE, st);
     HIPC(hipMemcpyAsync(h_shard, resmax, RES_SHARDS * SHARD_STRIDE * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -1460,7 +1493,8 @@ class Solver {
       check_launch("centers_stats");
     }
     if (P.ordering == CFD_ORDER_LEX)
-      seq_sum_kernel<<<1, 64, 0, st>>>(S[0].g, C, S[0].b[B_UC], S[0].b[B_VC], 1, total + 1);
+      for (size_t q = 0; q < S.size(); ++q)
+        seq_sum_kernel<<<1, 64, 0, st>>>(S[q].g, C, S[q].b[B_UC], S[q].b[B_VC], 1, total + 1, q > 0);
     else
       sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total + 1);
     check_launch("sum_partials");

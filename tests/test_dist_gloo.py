@@ -151,3 +151,153 @@ def test_two_rank_strips_equal_single_domain(world, nx, ny, spl):
     for rank, j0, j1, strip, res_hist in out:
         assert np.array_equal(strip, p[j0:j1 + 1])
         assert res_hist == hist
+
+
+# ---- the default rank launch: 4 sweeps with the proof-mode test ----
+
+def proof_ratio(dmax, pin, F, tol, h, omega, ns):
+    """kernels.hpp proof_ratio (the launch kernel's form, P bounded per rank)."""
+    idx2 = 1.0 / (h * h)
+    K = 4.0 * idx2 * abs(1.0 - omega) / omega
+    P = 9.0**ns * (pin + h * h * F) * (1.0 + 2.0**-40)
+    margin = 2.0**-43 * (idx2 * P + F)
+    thr = (tol + margin) / K * (1.0 + 2.0**-38)
+    q = dmax / thr
+    return q if (q == q and q >= 0.0) else 0.0
+
+
+def black_moves(p_old, p_new, nx, ny, lo):
+    """max |p' - p| over the black four-neighbour cells (1 < i < nx, 1 <= j < ny)."""
+    jj, ii = np.meshgrid(np.arange(p_old.shape[0]) + lo, np.arange(p_old.shape[1]), indexing="ij")
+    m = (ii > 1) & (ii < nx) & (jj >= 1) & (jj < ny) & (((ii + jj) & 1) == 1)
+    m[0, :] = m[-1, :] = False
+    return float(np.abs(np.where(m, p_new - p_old, 0.0)).max())
+
+
+def _solve_ranks(rank, world, nx, ny, f_full, omega, tol, cap, chunk, exchange, allmax):
+    """Solver::solve on one rank: launches of 4 proof-mode sweeps, the window of
+    each launch tested after it (all-reduced ratio > 1: proven); an iteration
+    the proof leaves open restarts the solve at that launch with exact 3-sweep
+    launches (all-reduced max-norm residual <= tol: the reference stops) for
+    `chunk` launches, then proof mode again. Returns the owned rows, the stop
+    iteration and the launch indices of the fallbacks."""
+    h = 1.0 / nx
+    j0, j1 = strip_rows(rank, world, ny)
+    lo = j0 - HALO
+    rows = np.arange(lo, j1 + HALO + 1)
+    valid = (rows >= 0) & (rows <= ny + 1)
+    f = np.zeros((len(rows), nx + 2)); f[valid] = f_full[rows[valid]]
+    F = float(np.abs(f_full[1:ny + 1, 1:nx + 1]).max())
+    p = np.zeros_like(f)
+    k, m, proof_from, fallbacks = 0, 0, 0, []
+    alone = 0  # sweeps this rank alone could not prove but the all-reduced ratio did
+    while k < cap:
+        proof = m >= proof_from
+        n = min(4 if proof else 3, cap - k)
+        exchange(p)
+        pin = float(np.abs(p).max())
+        pn, stop, open_k = p, None, None
+        for s in range(n):
+            prev = pn
+            pn = rb_iteration(pn, f, nx, ny, omega, h, lo, None)
+            if proof and n >= 3:
+                ql = proof_ratio(black_moves(prev, pn, nx, ny, lo), pin, F, tol, h, omega, n)
+                q = allmax(ql)
+                alone += int(not ql > 1.0 and q > 1.0)
+                if not q > 1.0 and open_k is None:
+                    open_k = k + s + 1
+            else:
+                r = allmax(residual(pn, f, nx, ny, h, lo)[HALO:-HALO].max())
+                if not r > tol and stop is None and open_k is None:
+                    stop = k + s + 1
+                    pstop = pn.copy()
+        if open_k is not None:  # exact evaluation from this launch's (intact) input
+            fallbacks.append(m)
+            proof_from = m + chunk
+            continue  # same m, same k, now exact (p is this launch's input: nothing was written)
+        if stop is not None:
+            pn = pstop
+            k = stop
+            p[HALO:-HALO] = pn[HALO:-HALO]
+            break
+        k += n
+        m += 1
+        p[HALO:-HALO] = pn[HALO:-HALO]
+        if rank == 0:
+            p[:HALO] = pn[:HALO]
+        if rank == world - 1:
+            p[-HALO:] = pn[-HALO:]
+    return j0, j1, p[HALO:-HALO].copy(), k, fallbacks, alone
+
+
+def _proof_worker(rank, world, port, q, nx, ny, tol, cap, chunk):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    try:
+        def exchange(p):
+            if rank > 0:
+                dist.send(torch.from_numpy(p[HALO:2 * HALO].copy()), rank - 1)
+                buf = torch.empty((HALO, p.shape[1]), dtype=torch.float64); dist.recv(buf, rank - 1)
+                p[:HALO] = buf.numpy()
+            if rank < world - 1:
+                buf = torch.empty((HALO, p.shape[1]), dtype=torch.float64); dist.recv(buf, rank + 1)
+                dist.send(torch.from_numpy(p[-2 * HALO:-HALO].copy()), rank + 1)
+                p[-HALO:] = buf.numpy()
+
+        q.put((rank,) + _solve_ranks(rank, world, nx, ny, _proof_source(nx, ny), 1.8, tol, cap, chunk, exchange,
+                                     lambda v: max_over_ranks(dist, v)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _proof_source(nx, ny):
+    """A source on the upper rank's rows only: the lower rank's own black moves
+    stay far below the threshold for the first launches, so a rank deciding
+    alone would fall back there; the all-reduced ratio decides for both."""
+    rng = np.random.default_rng(3)
+    f = np.zeros((ny + 2, nx + 2))
+    f[ny // 2 + 4:ny + 1, 1:nx + 1] = rng.standard_normal((ny - ny // 2 - 3, nx)) * 50.0
+    return f
+
+
+@pytest.mark.parametrize("tol,cap", [(20.0, 400), (12.0, 400), (1e9, 400), (0.0, 37)])
+def test_two_rank_proof_launches_equal_single_domain(tol, cap):
+    """Two gloo ranks of 64 rows (the same 8-row halos as the GPU's 512-row
+    strips): the 4-sweep proof-mode launch, ratios
+    all-reduced (max) like the GPU's ring slots, a fallback taken by both ranks
+    at the same launch, exact launches for a chunk, proof again. The stop
+    iteration and the fields must equal one domain with an exact residual test
+    every sweep (the reference's loop in red-black order); a capped solve never
+    falls back after its first launches."""
+    world, nx, ny, chunk = 2, 40, 128, 2
+    ctx = mp.get_context("spawn")
+    qq = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_proof_worker, args=(r, world, port, qq, nx, ny, tol, cap, chunk))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    out = sorted(qq.get(timeout=300) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    # one domain, exact residual after every sweep
+    f = _proof_source(nx, ny)
+    p = np.zeros_like(f)
+    k = 0
+    while k < cap:
+        p = rb_iteration(p, f, nx, ny, 1.8, 1.0 / nx, 0, None)
+        k += 1
+        if not residual(p, f, nx, ny, 1.0 / nx, 0).max() > tol:
+            break
+    fb = [o[5] for o in out]
+    assert fb[0] == fb[1], "both ranks fall back at the same launches"
+    for rank, j0, j1, strip, kk, _, _ in out:
+        assert kk == k
+        assert np.array_equal(strip, p[j0:j1 + 1])
+    if tol == 1e9:
+        assert k == 1  # (the first iteration already meets it)
+    if 0.0 < tol < 1e9:
+        assert len(fb[0]) >= 1  # converging: the last iterations are evaluated exactly
+        assert out[0][6] > 0  # the lower rank alone would have fallen back earlier

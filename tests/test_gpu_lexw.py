@@ -164,3 +164,92 @@ def test_sampled_rows_open_iterations_exact(seed):
         assert_bits(g.field("p"), o.field("p"), f"sampled lexw seed {seed} solve {rep}")
         if rep == 0:
             assert g.timing().proof_fallbacks >= 1  # a converging sampled solve always ends open
+
+
+# ---- the channel (configs[2]) in the reference's order: lexw.hpp lxo_row ----
+
+def random_field(cp, seed, scale=1.0):
+    rng = np.random.default_rng(seed)
+    return rng.standard_normal((cp.ny + 2, cp.nx + 2)) * scale
+
+
+def solve_channel(cp, f, p0, strips=1):
+    """One solverPressurePoisson from a given source and initial pressure
+    (ghosts included: the reference's first sweep reads them as stored)."""
+    g = C.ChannelSolver(cp, ordering="lex", n_strips=strips)
+    o = O.Oracle(cp, ordering=O.LEX)
+    g.set_field("src", f)
+    g.set_field("p", p0)
+    o.field("src")[...] = f
+    o.field("p")[...] = p0
+    res_g = g.solverPressurePoisson()
+    res_o = o.poisson()
+    return g, o, res_g, res_o
+
+
+@pytest.mark.parametrize("nx,ny,K,strips", [(93, 31, 37, 1), (300, 130, 25, 1), (129, 257, 1, 1), (129, 257, 2, 1),
+                                            (257, 64, 113, 1), (200, 150, 41, 2), (200, 150, 41, 3), (224, 40, 17, 1),
+                                            (225, 41, 18, 1)])
+def test_channel_capped_solve_bitexact(nx, ny, K, strips):
+    """Capped solves (the reference caps at 4096x512): ghosts refreshed in the
+    skew, the Dirichlet outlet, arbitrary initial ghosts, odd and even widths
+    (the outlet ghost in either slot), tile-edge widths, strips."""
+    cp = C.make_params("channel", nx=nx, ny=ny, max_iters=K)
+    f = random_field(cp, 5, 10.0)
+    p0 = random_field(cp, 6)
+    g, o, rg, ro = solve_channel(cp, f, p0, strips)
+    assert rg[0] == ro[0] == K
+    assert rg == ro
+    assert_bits(g.field("p"), o.field("p"), f"channel lexw p {nx}x{ny} K={K} strips={strips}")
+
+
+def test_channel_converging_solve_bitexact():
+    """The reference's own channel (93x31) after one predictor step converges;
+    the sampled rows leave the last iterations open and the exact check / the
+    continuation must land on the reference's count."""
+    cp = C.reference_defaults("channel")
+    g = C.ChannelSolver(cp, ordering="lex")
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.velocity_bc(False)
+    for s in (g, ):
+        s.computeTentativeVelocities()
+        s.applyTentativeBoundaryConditions()
+        s.buildSourceTerm()
+    o.tentative()
+    o.velocity_bc(True)
+    o.source()
+    ig, rg = g.solverPressurePoisson()
+    io, ro = o.poisson()
+    assert 10 < io < cp.max_iters
+    assert (ig, rg) == (io, ro)
+    assert_bits(g.field("p"), o.field("p"), "channel converged p")
+
+
+@pytest.mark.parametrize("case", ["reference", "wide"])
+def test_channel_whole_steps_bitexact(case):
+    """Whole channel steps in the reference's order (the source's mean removed
+    by the sequential sum), against the reference loop restated."""
+    if case == "reference":
+        cp, steps = C.reference_defaults("channel"), 12
+    else:
+        cp, steps = C.make_params("channel", re=1000.0, nx=384, ny=64, max_iters=200), 3
+    g = C.ChannelSolver(cp, ordering="lex")
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.velocity_bc(False)
+    for k in range(steps):
+        assert g.step() == o.step(), k
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"channel {case} {name}")
+
+
+def test_channel_4096x512_step_bitexact_capped():
+    """BASELINE configs[2] (channel Re=1000, 4096x512): whole timesteps in the
+    reference's order, capped, bit for bit."""
+    cp = C.make_params("channel", re=1000.0, nx=4096, ny=512, max_iters=30)
+    g = C.ChannelSolver(cp, ordering="lex")
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.velocity_bc(False)
+    for k in range(2):
+        assert g.step() == o.step(), k
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"channel 4096x512 {name}")
