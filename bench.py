@@ -95,7 +95,7 @@ def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch
     import torch
 
     s = C.solver_for(cp, device=device, check_every=check_every, ordering="lex",
-                     sweeps_per_launch=args.sweeps_per_launch or 3)
+                     sweeps_per_launch=args.sweeps_per_launch)
     if args.case == "cavity":
         s.applyBoundaryConditions()
     s.step()  # warmup
@@ -113,7 +113,9 @@ def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch
     return {"ordering": "lex", "value": round(tm.poisson_cell_updates / el / 1e6, 2), "unit": "MLUPS",
             "ms_per_step": round(el / args.lex_steps * 1e3, 3), "steps": args.lex_steps,
             "sor_iterations_per_step": iters,
-            "kernel": f"poisson_lexw_kernel<{args.sweeps_per_launch or 3}>",
+            "kernel": f"poisson_lexw_kernel<{args.case},{round(tm.poisson_sweeps / max(tm.poisson_launches, 1))},"
+                      f"sampled>",
+            "sweeps_per_launch": round(tm.poisson_sweeps / max(tm.poisson_launches, 1), 3),
             "launches_per_step": round(tm.poisson_launches / args.lex_steps, 1),
             "steady_launches_per_step": round(tm.poisson_steady_launches / args.lex_steps, 1),
             "steady_launch_us": round(steady_ms * 1e3, 2) if tm.poisson_steady_launches else None,

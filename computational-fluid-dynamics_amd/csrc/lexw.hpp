@@ -54,6 +54,15 @@ constexpr int LEXW_SHARDS = 8;
 #endif
 #define CFD_LEXW_MIN_WAVES(NS) ((NS) <= 2 ? CFD_LEXW_W2 : CFD_LEXW_W3)  // copies of the exceedance bitset (by block, ~XCD)
 
+// Output columns per wave. A value is exact after s half-sweeps on the wave's
+// columns [s, 127-s]; the residual evaluated in half-sweep h reads its east
+// neighbour's NEW value (column x+1 after h). At 4 sweeps (h up to 8) the last
+// output column must therefore be 127-9 = 118: output columns 8..117 (110,
+// lanes 4..58; 10-column right halo). Up to 3 sweeps: 8..119 (112, lanes
+// 4..59), the red-black kernels' PAIR_TWC. Rows likewise: a strip's stored
+// 8-row halo serves up to 3 sweeps (Solver::lexw_ns keeps strips at 3).
+__host__ __device__ constexpr int lexw_twc(int ns) { return ns >= 4 ? 110 : PAIR_TWC; }
+
 // Ramp-launch tiling: bands of `th` rows from row `row0`; band b holds the
 // column tiles ca..cb (the ones its rows touch), numbered from first: band[b]
 // = first << 16 | ca << 8 | cb. Waves map to tiles band by band, column tiles
@@ -519,12 +528,13 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
 // half-sweeps later than their position (lxo_row).
 __host__ __device__ inline void lexw_rows(const Geo& g, int H0, int K, int ns, int ct, int* lo, int* hi,
                                           bool open = false) {
+  const int twc = lexw_twc(ns);
   if (!open) {
-    const int cmin = max(ct * PAIR_TWC, 1), cmax = min(ct * PAIR_TWC + PAIR_TWC - 1, g.nx);
+    const int cmin = max(ct * twc, 1), cmax = min(ct * twc + twc - 1, g.nx);
     *lo = max(g.j0, H0 - 2 * ns - 2 * (K - 1) - cmax);
     *hi = min(g.j1, H0 + 2 * ns - 1 - cmin);
   } else {
-    const int cmin = max(ct * PAIR_TWC, 0), cmax = min(ct * PAIR_TWC + PAIR_TWC - 1, g.nx + 1);
+    const int cmin = max(ct * twc, 0), cmax = min(ct * twc + twc - 1, g.nx + 1);
     *lo = max(g.wj0, H0 - 2 * ns - 2 * (K - 1) - cmax - 2);
     *hi = min(g.wj1, H0 + 2 * ns - 1 - cmin);
   }
@@ -592,7 +602,8 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     y0 = r0 ? pl.lo0 + band * th : pl.lo1 + (band - nb0) * th;
     y1 = min(y0 + th, r0 ? pl.hi0 : pl.hi1);
   }
-  const int c0 = ctile * PAIR_TWC - CH;
+  constexpr int TWC = lexw_twc(NS);
+  const int c0 = ctile * TWC - CH;
   const int gi = c0 + 2 * lane;
   if (y0 >= y1) return;
 
@@ -619,7 +630,7 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   x.rmin = max(g.row_lo, 0);
   x.rmax = min(g.row_lo + g.nrows - 1, g.ny + 1);
   x.pair_ok = gi >= 0 && gi + 1 < g.pitch;
-  x.out_lane = x.pair_ok && lane >= CH / 2 && lane < 64 - CH / 2;
+  x.out_lane = x.pair_ok && lane >= CH / 2 && lane < CH / 2 + TWC / 2;
   x.icol_a = gi >= 1 && gi <= g.nx;
   x.icol_b = gi + 1 >= 1 && gi + 1 <= g.nx;
   x.open_a = x.open_b = true;

@@ -196,10 +196,14 @@ class Solver {
   bool use_lexw() const {
     return P.ordering == CFD_ORDER_LEX && (P.case_id == CFD_CAVITY || P.case_id == CFD_CHANNEL);
   }
+  // sweeps per reference-order launch: 4 (auto) on one strip; strips keep 3
+  // (their 8-row halos serve up to 3, lexw.hpp lexw_twc); the cavity also 1-3
   int lexw_ns() const {
-    if (P.case_id != CFD_CAVITY) return 3;
-    return P.sweeps_per_launch >= 1 ? P.sweeps_per_launch : 3;
+    const int ns = (P.case_id != CFD_CAVITY || P.sweeps_per_launch < 1) ? 4 : P.sweeps_per_launch;
+    return S.size() > 1 ? std::min(ns, 3) : ns;
   }
+  // rows one lexw wave marches beyond its band: the pipeline (2NS+1 each side) + parity row
+  static int lexw_extra(int ns) { return 2 * (2 * ns + 1) + 1; }
 
   // Rayleigh-Benard: the cavity's projection (P.case_id is set to CFD_CAVITY,
   // u_ref 0 = lid at rest) plus the temperature stage on tcur/tnext.
@@ -260,7 +264,9 @@ class Solver {
       if (use_lexw()) {
         int lps = 0;
         if (P.case_id == CFD_CHANNEL)
-          HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<CHANNEL, 3, false, true>, 256, 0));
+          HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<CHANNEL, 4, false, true>, 256, 0));
+        else if (lexw_ns() == 4)
+          HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<CAVITY, 4, false, true>, 256, 0));
         else if (lexw_ns() == 1)
           HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<CAVITY, 1, false>, 256, 0));
         else if (lexw_ns() == 2)
@@ -430,8 +436,9 @@ class Solver {
       throw Error(CFD_E_ARG, "sweeps_per_launch must be 0 (auto), 1, 2, 3 or 4");
     if (P.sweeps_per_launch >= 3 && P.case_id != CFD_CAVITY && P.ordering == CFD_ORDER_RB)
       throw Error(CFD_E_ARG, "three or four red-black sweeps per launch are implemented for the cavity only");
-    if (P.sweeps_per_launch == 4 && P.ordering == CFD_ORDER_LEX)
-      throw Error(CFD_E_ARG, "the lexicographic-order kernel runs 1, 2 or 3 sweeps per launch");
+    if (P.sweeps_per_launch >= 1 && P.sweeps_per_launch != 4 && P.ordering == CFD_ORDER_LEX &&
+        P.case_id != CFD_CAVITY && P.case_id != CFD_RAYLEIGH_BENARD)
+      throw Error(CFD_E_ARG, "the open cases' lexicographic-order kernel runs 4 sweeps per launch (0: auto)");
     if (P.sweeps_per_launch == 4 && P.ordering == CFD_ORDER_RB && P.proof_test == CFD_OFF)
       throw Error(CFD_E_ARG, "four red-black sweeps per launch need the proof-mode test (proof_test != CFD_OFF)");
     for (int sw : {P.proof_test, P.small_solve, P.overlap})
@@ -604,10 +611,10 @@ class Solver {
   // a multiple of 10. The two boundary column tiles march slower (masks):
   // shorter bands, pair_edge_pct % of the interior march.
   PairPlan multi_plan(int lo0, int hi0, int lo1, int hi1, int waves, int n, int max_th = 1 << 30,
-                      int edge_pct = -1) const {
+                      int edge_pct = -1, int twc = PAIR_TWC, int ex = -1) const {
     if (edge_pct < 0) edge_pct = pair_edge_pct;
     PairPlan pl{};
-    pl.ctiles = (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC;
+    pl.ctiles = (P.nx + 2 + twc - 1) / twc;
     pl.lo0 = lo0; pl.hi0 = hi0; pl.lo1 = lo1; pl.hi1 = hi1;
     if (P.case_id == CFD_BACKSTEP) {
       // interior column tiles across the step's column (neither left of it,
@@ -625,7 +632,7 @@ class Solver {
     const int rows = (hi0 - lo0) + (hi1 - lo1);
     const int ne = plan_edge_tiles(pl);
     const int rmax = std::max(hi0 - lo0, hi1 - lo1);
-    const int ex = march_extra(n);
+    if (ex < 0) ex = march_extra(n);
     auto nbands = [](int lo, int hi, int t) { return hi > lo ? (hi - lo + t - 1) / t : 0; };
     int nb = std::max(1, std::min(waves / std::max(1, pl.ctiles), (rows + march_min_th - 1) / march_min_th));
     nb = std::max(nb, (rows + max_th - 1) / max_th);
@@ -881,7 +888,7 @@ class Solver {
         }
       }
       if (rh < rl) return;
-      const int ex = march_extra(ns);
+      const int ex = lexw_extra(ns);
       auto build = [&](int th) {  // fills rp for band height th; returns the tile count
         rp.th = th;
         rp.row0 = rl;
@@ -915,9 +922,15 @@ class Solver {
 #define CFD_LEXW_LAUNCH(CASE, NS, R, SM) \
   poisson_lexw_kernel<CASE, NS, R, SM><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl, rp)
     // (sampled residual rows: the 3-sweep kernels, the default; 1 and 2 sweeps evaluate every row)
-    if (P.case_id == CFD_CHANNEL) {
+    if (P.case_id == CFD_CHANNEL && ns == 3) {  // (strips)
       if (sample) { if (steady) CFD_LEXW_LAUNCH(CHANNEL, 3, false, true); else CFD_LEXW_LAUNCH(CHANNEL, 3, true, true); }
       else { if (steady) CFD_LEXW_LAUNCH(CHANNEL, 3, false, false); else CFD_LEXW_LAUNCH(CHANNEL, 3, true, false); }
+    } else if (P.case_id == CFD_CHANNEL) {
+      if (sample) { if (steady) CFD_LEXW_LAUNCH(CHANNEL, 4, false, true); else CFD_LEXW_LAUNCH(CHANNEL, 4, true, true); }
+      else { if (steady) CFD_LEXW_LAUNCH(CHANNEL, 4, false, false); else CFD_LEXW_LAUNCH(CHANNEL, 4, true, false); }
+    } else if (ns == 4) {
+      if (sample) { if (steady) CFD_LEXW_LAUNCH(CAVITY, 4, false, true); else CFD_LEXW_LAUNCH(CAVITY, 4, true, true); }
+      else { if (steady) CFD_LEXW_LAUNCH(CAVITY, 4, false, false); else CFD_LEXW_LAUNCH(CAVITY, 4, true, false); }
     } else if (ns == 1) { if (steady) CFD_LEXW_LAUNCH(CAVITY, 1, false, false); else CFD_LEXW_LAUNCH(CAVITY, 1, true, false); }
     else if (ns == 2) { if (steady) CFD_LEXW_LAUNCH(CAVITY, 2, false, false); else CFD_LEXW_LAUNCH(CAVITY, 2, true, false); }
     else if (sample) { if (steady) CFD_LEXW_LAUNCH(CAVITY, 3, false, true); else CFD_LEXW_LAUNCH(CAVITY, 3, true, true); }
@@ -947,12 +960,12 @@ class Solver {
     // (i+j = 2) is the first: launches from m_full evaluate iterations >=
     // kexact everywhere. Replays (no tests) use the sampled kernel throughout.
     // (kexact >= K: no iteration the solve tests is evaluated everywhere)
-    const int m_full = (!tests || kexact >= K) ? INT32_MAX : (ns == 3) ? (2 * kexact - 1) / (2 * ns) : 0;
+    const int m_full = (!tests || kexact >= K) ? INT32_MAX : (ns >= 3) ? (2 * kexact - 1) / (2 * ns) : 0;
     std::vector<PairPlan> plans(S.size());
     for (size_t q = 0; q < S.size(); ++q)
       plans[q] = multi_plan(S[q].g.wj0, S[q].g.wj1 + 1, 0, 0, resident_lexw_waves / (int)S.size(), ns,
-                            96,  // (a wave's march <= 118 rows: its iterations fit one 64-bit mask)
-                            lexw_edge_pct);
+                            96,  // (a wave's march <= 96 + 19 rows: its iterations fit one 64-bit mask)
+                            lexw_edge_pct, lexw_twc(ns), lexw_extra(ns));
     // steady launches: every cell active in every half-sweep of the launch and
     // of the previous one's last (nx+ny+1 <= H0 <= 2K-2NS+1, H0 = 2 + 2NS m)
     const int ms0 = (P.nx + P.ny - 1 + 2 * ns - 1) / (2 * ns), ms1 = floordiv(2 * K - 2 * ns - 1, 2 * ns);
@@ -1094,7 +1107,7 @@ class Solver {
     }
     lex_reset_tests();
     HIPC(hipEventRecord(ev_a, st));
-    const int kexact = (ns != 3) ? 1 : (lex_hint > 0 && lex_hint < K) ? std::max(1, lex_hint - 64) : K;
+    const int kexact = (ns < 3) ? 1 : (lex_hint > 0 && lex_hint < K) ? std::max(1, lex_hint - 64) : K;
     int iters = K, kstop = -1, code = 0, fin = base;
     if (K > 0) {
       const int launched = run_lexw(base, K, true, kexact, 0, &kstop, &code, true);

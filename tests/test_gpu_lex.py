@@ -77,9 +77,10 @@ def test_lex_vtk_frame_byte_identical(tmp_path):
     assert hashlib.sha256(fn.read_bytes()).hexdigest() == LOGS["cavity"]["vtk_sha256"]["100"]
 
 
-def test_open_case_lex_rejects_strips():
-    """The open cases' reference order runs in one workgroup (poisson_lex_kernel):
-    one strip only. (The cavity's runs on strips: tests/test_gpu_lexw.py.)"""
+def test_step_lex_rejects_strips():
+    """The backwards step's reference order runs in one workgroup
+    (poisson_lex_kernel): one strip only. (The cavity's and the channel's run
+    on strips: tests/test_gpu_lexw.py.)"""
     with pytest.raises(C._lib.CfdError if hasattr(C, "_lib") else Exception):
-        g = C.ChannelSolver(C.reference_defaults("channel"), ordering="lex", n_strips=2)
+        g = C.BackwardsStepSolver(C.reference_defaults("backwards_step"), ordering="lex", n_strips=2)
         g.step()

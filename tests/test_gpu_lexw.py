@@ -7,7 +7,9 @@ tests/test_oracle_golden.py).
 Bars: iteration counts equal, reported residual equal, every field equal bit
 for bit — at capped sweep counts where the solve runs into the cap (the
 BASELINE sizes), at converging solves (the early stop and its replay), on
-1..3 strips, for 1, 2 and 3 sweeps per launch.
+1..3 strips, for 1 to 4 sweeps per launch (4, the default on one strip,
+with 110-column tiles: lexw.hpp lexw_twc; widths 219/220 put the last
+columns on a 110-column tile edge).
 """
 from __future__ import annotations
 
@@ -38,8 +40,9 @@ def random_source(cp, seed=5, scale=10.0):
     return f
 
 
-@pytest.mark.parametrize("spl", [1, 2, 3])
-@pytest.mark.parametrize("nx,ny,K", [(40, 24, 37), (300, 130, 25), (129, 257, 1), (129, 257, 2), (257, 64, 113)])
+@pytest.mark.parametrize("spl", [1, 2, 3, 4])
+@pytest.mark.parametrize("nx,ny,K", [(40, 24, 37), (300, 130, 25), (129, 257, 1), (129, 257, 2), (257, 64, 113),
+                                     (219, 40, 29), (220, 41, 30)])
 def test_capped_solve_bitexact(nx, ny, K, spl):
     cp = C.make_params("cavity", nx=nx, ny=ny, max_iters=K)
     f = random_source(cp)
@@ -58,7 +61,7 @@ def test_capped_solve_strips_bitexact(strips):
     assert_bits(g.field("p"), o.field("p"), f"lexw strips={strips}")
 
 
-@pytest.mark.parametrize("spl", [2, 3])
+@pytest.mark.parametrize("spl", [2, 3, 4])
 def test_converging_solve_stops_at_reference_iteration(spl):
     """The reference's own 63² cavity: a realistic source (one predictor step)
     converges in a few hundred sweeps; the stop is detected up to (nx+ny)/2
