@@ -121,7 +121,9 @@ def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch
             "steady_launch_us": round(steady_ms * 1e3, 2) if tm.poisson_steady_launches else None,
             "steady_achieved_GBs": round(achieved, 1) if achieved else None,
             "steady_frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "steady_traffic": pmc_traffic("r2_lexw_pmc.json", cp.nx, cells_per_launch // (cp.nx + 2), 3)}
+            "steady_traffic": pmc_traffic(f"r3_pmc_{args.case}_lex_{cp.nx}x{cells_per_launch // (cp.nx + 2) - 2}.json",
+                                          cp.nx, cells_per_launch // (cp.nx + 2),
+                                          round(tm.poisson_sweeps / max(tm.poisson_launches, 1)))}
 
 
 def pmc_traffic(name: str, nx: int, rows: int, sweeps: int):
@@ -246,7 +248,7 @@ def main() -> int:
         g0, g1 = solver.owned_rows()
         wrows = (g1 - g0 + 1) + (1 if g0 == 1 else 0) + (1 if g1 == cp.ny else 0)
         cells_per_launch = wrows * (cp.nx + 2)
-        lexw = args.ordering == "lex" and kcase_of(args.case) == "cavity"
+        lexw = args.ordering == "lex" and kcase_of(args.case) in ("cavity", "channel")
         if lexw and tm.poisson_steady_launches > 0:
             # lexicographic order: the launches with every cell active (the
             # ramps at both ends of a solve skip or mask part of the grid)
@@ -260,18 +262,15 @@ def main() -> int:
         # the same launch measured as if each sweep streamed its own 24 B/cell
         # (the unfused algorithm's traffic): the temporal-blocking gain
         effective = achieved * sweeps_per_launch
-        traffic = None if lexw else pmc_traffic("poisson_pmc.json", cp.nx, wrows, round(sweeps_per_launch))
-        if lexw:
-            traffic = pmc_traffic("r2_lexw_pmc.json", cp.nx, wrows, round(sweeps_per_launch))
+        # HBM bytes per launch from the committed PMC pass of the same workload (profiles/)
+        traffic = pmc_traffic(f"r3_pmc_{args.case}_{args.ordering}_{cp.nx}x{wrows - 2}.json", cp.nx, wrows,
+                              round(sweeps_per_launch))
         mlups = updates / elapsed / 1e6
         kcase = kcase_of(args.case)
         # red-black cavity launches: proof-mode convergence test (DESIGN.md
         # §2; --proof-test off evaluates the residual in every sweep)
         proof = (not lexw and kcase == "cavity" and round(sweeps_per_launch) >= 3
                  and args.proof_test != "off")
-        if proof:
-            traffic = pmc_traffic(f"r2_proof{round(sweeps_per_launch)}_pmc.json", cp.nx, wrows,
-                                  round(sweeps_per_launch))
         rows_here = g1 - g0 + 1
         per_gpu = (f"{cp.nx}x{rows_here} fp64 cells per GPU (global {cp.nx}x{cp.ny} split over {n_gpus} GPUs)"
                    if strong else f"{cp.nx}x{args.ny} fp64 cells per GPU (global {cp.nx}x{cp.ny})")
@@ -311,7 +310,7 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": (f"poisson_lexw_kernel<{round(sweeps_per_launch)}>" if lexw
+                "kernel": (f"poisson_lexw_kernel<{kcase},{round(sweeps_per_launch)},sampled> (steady launches)" if lexw
                            else f"poisson_multi_kernel<{kcase},{round(sweeps_per_launch)},proof>" if proof
                            else f"poisson_multi_kernel<{kcase},3>" if sweeps_per_launch > 2.5
                            else f"poisson_multi_kernel<{kcase},2>" if sweeps_per_launch > 1.5
@@ -327,7 +326,8 @@ def main() -> int:
             log("timing the CPU baseline ...")
             line["cpu_baseline"] = cpu_baseline(cp.nx, cp.ny, args.cpu_seconds, args.case)
 
-    if rank == 0 and world == 1 and args.lex_steps > 0 and args.ordering == "rb" and kcase_of(args.case) == "cavity":
+    if (rank == 0 and world == 1 and args.lex_steps > 0 and args.ordering == "rb"
+            and kcase_of(args.case) in ("cavity", "channel")):
         line["reference_order"] = reference_order(C, cp, args, local_rank, check_every, cells_per_launch)
     if rank == 0:
         print(json.dumps(line), flush=True)

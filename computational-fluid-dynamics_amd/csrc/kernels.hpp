@@ -1747,57 +1747,48 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
 // for the bit-identical (lexicographic) mode: mode 0 = sum of the source
 // (channel-01.cpp:622-624, backwards_step-01.cpp fluid cells), mode 1 = kinetic
 // energy 0.5*(u_c^2+v_c^2) (cavity-01.cpp:750-755). The rounding chain is
-// inherently sequential, so one lane adds; the wave only feeds it: each round
-// the 64 lanes stage SEQ_CHUNK terms (in order) in LDS, then lane 0 adds them
-// while the next chunk's loads are in flight. Strips are summed in order, each
-// launch continuing from the previous strip's partial sum (accumulate).
-constexpr int SEQ_CHUNK = 1024;
+// inherently sequential: one wave loads SEQ_PER x 64 terms per round
+// (coalesced, the next round in flight) and adds them in order as wave-uniform
+// values (readlane), one dependent add per term. A solid cell contributes
+// -0.0, which leaves every sum unchanged (x + -0.0 == x, -0.0 + -0.0 == -0.0),
+// as skipping it does. Strips are summed in order, each launch continuing from
+// the previous strip's partial sum (accumulate).
+constexpr int SEQ_PER = 8;
 __global__ __launch_bounds__(64) void seq_sum_kernel(Geo g, Coef c, const double* __restrict__ a,
                                                      const double* __restrict__ b, int mode, double* __restrict__ out,
                                                      int accumulate) {
-  __shared__ double buf[SEQ_CHUNK];
-  __shared__ unsigned char use_buf[SEQ_CHUNK];  // 0: a solid cell, no term
   const int lane = threadIdx.x;
   const int ja = max(g.j0, 1), jb = min(g.j1, g.ny);
   const int nx = g.nx;
   const long long n = (long long)max(0, jb - ja + 1) * nx;  // cells in loop order: q -> (ja + q / nx, 1 + q % nx)
-  constexpr int PER = SEQ_CHUNK / 64;
-  double v[PER];
-  bool u[PER];
-  auto load = [&](long long q0) {  // this lane's terms q0 + lane + 64 k (0 for solid cells / past the end)
+  constexpr int ROUND = 64 * SEQ_PER;
+  auto load = [&](long long q0, double (&v)[SEQ_PER]) {  // term q0 + 64 k + lane in v[k]
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const long long q = q0 + lane + 64 * k;
-      double t = 0.0;
-      bool use = false;
+    for (int k = 0; k < SEQ_PER; ++k) {
+      const long long q = q0 + 64 * k + lane;
+      double t = -0.0;
       if (q < n) {
         const int j = ja + (int)(q / nx), i = 1 + (int)(q % nx);
-        use = is_fluid(c, nx, g.ny, j, i);
         const size_t o = at(g, j, i);
-        t = (mode == 0) ? a[o] : 0.5 * (a[o] * a[o] + b[o] * b[o]);
+        const double tv = (mode == 0) ? a[o] : 0.5 * (a[o] * a[o] + b[o] * b[o]);
+        t = is_fluid(c, nx, g.ny, j, i) ? tv : -0.0;
       }
       v[k] = t;
-      u[k] = use;  // a solid cell is skipped by the reference
     }
   };
   double s = accumulate ? out[0] : 0.0;
-  load(0);
-  for (long long q0 = 0; q0 < n; q0 += SEQ_CHUNK) {
+  double v[SEQ_PER], w[SEQ_PER];
+  load(0, v);
+  for (long long q0 = 0; q0 < n; q0 += ROUND) {
+    if (q0 + ROUND < n) load(q0 + ROUND, w);  // in flight during the chain
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      buf[lane + 64 * k] = v[k];
-      use_buf[lane + 64 * k] = u[k] ? 1 : 0;
+    for (int k = 0; k < SEQ_PER; ++k) {
+      const int hi = __double2hiint(v[k]), lo = __double2loint(v[k]);
+      for (int l = 0; l < 64; ++l)
+        s += __hiloint2double(__builtin_amdgcn_readlane(hi, l), __builtin_amdgcn_readlane(lo, l));
     }
-    __syncthreads();
-    if (q0 + SEQ_CHUNK < n) load(q0 + SEQ_CHUNK);  // in flight while lane 0 adds
-    if (lane == 0) {
-      const int cnt = (int)min((long long)SEQ_CHUNK, n - q0);
-      for (int k = 0; k < cnt; ++k) {
-        const double t = buf[k];
-        if (use_buf[k]) s += t;
-      }
-    }
-    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SEQ_PER; ++k) v[k] = w[k];
   }
   if (lane == 0) out[0] = s;
 }

@@ -61,7 +61,11 @@ constexpr int LEXW_SHARDS = 8;
 // lanes 4..58; 10-column right halo). Up to 3 sweeps: 8..119 (112, lanes
 // 4..59), the red-black kernels' PAIR_TWC. Rows likewise: a strip's stored
 // 8-row halo serves up to 3 sweeps (Solver::lexw_ns keeps strips at 3).
-__host__ __device__ constexpr int lexw_twc(int ns) { return ns >= 4 ? 110 : PAIR_TWC; }
+// At 5 sweeps (the cavity on one strip) the left halo grows to 10 columns
+// (output column 10 reads column 9 after 9 half-sweeps) and the right one to
+// 12: output columns 10..115 (106, lanes 5..57).
+__host__ __device__ constexpr int lexw_twc(int ns) { return ns >= 5 ? 106 : ns == 4 ? 110 : PAIR_TWC; }
+__host__ __device__ constexpr int lexw_ch(int ns) { return ns >= 5 ? 10 : 8; }
 
 // Ramp-launch tiling: bands of `th` rows from row `row0`; band b holds the
 // column tiles ca..cb (the ones its rows touch), numbered from first: band[b]
@@ -82,6 +86,8 @@ struct LexCtl {
   int* stop;                 // [0] 1: the reference stops at iteration [1]; 2: iteration [1] left open
   int kexact;                // iterations >= kexact have every cell's residual evaluated (full
                              // launches); below it the bits come from sampled rows (LX_SAMPLE)
+  double* cscr;              // backwards step: the corner's south neighbour's deferred residual
+                             // across a launch boundary: {x-part, p_S, iteration} (lxo_row)
 };
 
 // slot k has a cell whose |residual| exceeds the tolerance (valid once every
@@ -137,6 +143,12 @@ __device__ __forceinline__ bool lexw_go_on(const LexCtl& L, int ka, int kb, bool
 // the march stalls the wave); the lanes' masks are merged along the
 // diagonals (iteration = Bd0 + t/2 - l) once per wave.
 
+// backwards step: the corner's south neighbour's pending residual (lxo_row)
+struct LxDefer {
+  double xp, ps;
+  int k;  // iteration of the pending residual, -1: none
+};
+
 template <int NS>
 struct LexRun {
   double2 w[NS][5];  // sweep S: rows R+2S .. R+2S+4
@@ -144,6 +156,7 @@ struct LexRun {
   double2 np[5];     // prefetched p_in rows R .. R-4
   double2 nf[5];     // prefetched f rows R+1 .. R-3
   unsigned long long mask;  // bit t/2: a residual of this lane's iteration Bd0 + t/2 - lane exceeds tol
+  LxDefer d;         // backwards step: the corner's south neighbour's pending residual (lxo_row)
 };
 
 // Per-wave context beyond WaveCtx: the launch's half-sweeps and the cap.
@@ -179,17 +192,20 @@ __device__ __forceinline__ double2 lx_ld(const WaveCtx<CAVITY>& x, const double*
 // which split the march loop into dozens of blocks, serialise its loads and
 // ran the ramp launches at half the steady kernel's speed.)
 constexpr int LX_ACT = 1;
+constexpr int LX_SAMPLE = 2;  // sampled residual rows (lx_res_row)
 struct LxAct {
   bool a, b, c;    // u, u-1, u-2 within [0, 2(K-1)]
   bool a2, b2;     // u-2, u-3: the same two half-sweeps later (open cases: the left / bottom ghosts)
+  unsigned u;      // (the step's corner logic: u == 0 is slot a's first iteration)
 };
-template <int MODE>
+template <int MODE, bool U = false>
 __device__ __forceinline__ LxAct lx_act(const LexCtx& lc, int gi, int R) {
-  if constexpr (!(MODE & LX_ACT)) return LxAct{true, true, true, true, true};
+  if constexpr (!(MODE & LX_ACT) && !U) return LxAct{true, true, true, true, true, 0u};
   const unsigned span = 2u * (unsigned)(lc.K - 1);
   unsigned u = (unsigned)(lc.H0 - 1 - R - gi);
   asm volatile("" : "+v"(u));  // (opaque: no loop splitting on the induction variable R)
-  return LxAct{u <= span, u - 1u <= span, u - 2u <= span, u - 2u <= span, u - 3u <= span};
+  if constexpr (!(MODE & LX_ACT)) return LxAct{true, true, true, true, true, u};
+  return LxAct{u <= span, u - 1u <= span, u - 2u <= span, u - 2u <= span, u - 3u <= span, u};
 }
 
 // SOR update (cavity-01.cpp:643-654) as pc*omm + om*sum in every cell. The
@@ -316,18 +332,52 @@ __device__ __forceinline__ void lx_row(const WaveCtx<CAVITY>& x, const LexCtx& l
 // the unmasked update (RC = false); the others choose per row (row-uniform).
 struct LxoCol {
   int ka, kb;  // per slot: 0 keep (outside the grid), 1 left ghost, 2 right ghost, 3 interior
+  int sa, sb;  // backwards step, per slot: column i < step_i (0), == step_i (1), > step_i (2)
 };
 __device__ __forceinline__ int lxo_kind(const WaveCtx<CAVITY>& x, int i) {
   return (i < 0 || i > x.g.nx + 1) ? 0 : (i == 0) ? 1 : (i == x.g.nx + 1) ? 2 : 3;
 }
+__device__ __forceinline__ int lxs_class(const WaveCtx<CAVITY>& x, int i) {
+  return (i < x.c.step_i) ? 0 : (i == x.c.step_i) ? 1 : 2;
+}
 
-template <int CASE, bool EDGE, bool RC>
-__device__ __forceinline__ double lxo_value(const WaveCtx<CAVITY>& x, int rk, int ck, double pc, double pW, double pE,
-                                            double pS, double pN, double fc) {
+// ---- backwards step (backwards_step-01.cpp:685-740, 872-939) ----
+//
+// Solid block: i <= si (step_i), j >= jb (inlet_jmax + 1). The reference
+// refreshes, after each sweep, the solid cells next to fluid to the mean of
+// their fluid neighbours (p_sum starts at 0.0, so one neighbour gives 0.0 + p,
+// which turns -0.0 into +0.0). In the skew (requires si >= 2, jb <= ny - 1):
+//  * bottom-row solids (jb, i < si): 0.0 + p_S, read by their south neighbour
+//    as p_prev: like the top ghost, a copy at their own skew time;
+//  * step-column solids (j > jb, si): 0.0 + p_E, read by their east neighbour
+//    as p_new: like the left ghost, two half-sweeps later;
+//  * the corner (jb, si) = ((0.0 + p_E) + p_S) / 2 with E = (jb, si+1),
+//    S = (jb-1, si): S's iteration k+1 and E's iteration k share a half-sweep,
+//    and S needs the corner of E(k). The march updates E's row first, so S's
+//    update computes the corner from E's new and its own old value, uses it as
+//    p_N and writes it into the corner's register, where E's next update and
+//    E's residual read it; the corner itself is kept (the final field's corner
+//    is refreshed after the solve, Solver::step_corner). S's own residual needs
+//    that corner too, one half-sweep after it is evaluated: its x part and p_S
+//    wait in registers (or, across a launch boundary, in LexCtl::cscr) until
+//    S's next update, which ORs the bit of its iteration directly. Sampled
+//    launches skip that one cell.
+//  * interior solids never change (both buffers hold them).
+// Residuals read the solids refreshed after the sweep: a bottom-row one is
+// updated in the residual's half-sweep (new value at hand); a step-column one
+// not yet, so the cell's own value stands in (0.0 + p_c).
+
+template <int CASE, bool EDGE, bool RC, bool STEP>
+__device__ __forceinline__ double lxo_value(const WaveCtx<CAVITY>& x, int rk, int ck, int rs, int cs, double pc,
+                                            double pW, double pE, double pS, double pN, double fc) {
   const double sor = sor_update<CASE>(x.c, 0, 0, 0, 0, pc, pW, pE, pS, pN, fc);
   if constexpr (!RC && !EDGE) return sor;
   double nv = sor;
-  if constexpr (EDGE) nv = (ck == 3) ? sor : (ck == 1) ? pE : (ck == 2) ? 0.0 : pc;
+  if constexpr (STEP) {  // row class rs: 0 below the block, 1 its bottom row, 2 above (row-uniform)
+    const double solid = (rs == 1) ? ((cs == 0) ? 0.0 + pS : pc) : ((cs == 0) ? pc : 0.0 + pE);
+    nv = (rs == 0 || cs == 2) ? sor : solid;
+  }
+  if constexpr (EDGE) nv = (ck == 3) ? nv : (ck == 1) ? pE : (ck == 2) ? 0.0 : pc;
   if constexpr (RC) {  // row kinds: 1 bottom ghost (copy N), 2 top ghost (copy S), 3 keep
     const double g = (rk == 1) ? pN : pS;
     if (EDGE) nv = (rk == 0) ? nv : (rk != 3 && ck == 3) ? g : pc;
@@ -336,27 +386,104 @@ __device__ __forceinline__ double lxo_value(const WaveCtx<CAVITY>& x, int rk, in
   return nv;
 }
 
-template <int CASE, int ROT, int JPAR, int COLOR, int MODE, bool EDGE, bool RC, bool STORE, bool RES>
-__device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxoCol& cc,
-                                        double2 (&W)[5], int j, int X, const LxAct& act, const double2& fc, int& exi) {
+template <int CASE, int ROT, int JPAR, int COLOR, int MODE, bool EDGE, bool RC, bool STORE, bool RES, bool FIRSTH,
+          bool LASTH>
+__device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L, const LxoCol& cc,
+                                        double2 (&W)[5], int j, int X, const LxAct& act, const double2& fc, int& exi,
+                                        LxDefer& d) {
+  // the step's general tiles (block boundary, ghosts): per-cell solid rules
+  constexpr bool STEP = CASE == BACKSTEP && EDGE && RC;
+  constexpr bool FULL = !(MODE & LX_SAMPLE);
   double2& m = W[LX_SLOT(X)];
-  const double2 nb = W[LX_SLOT(X + 1)], sb = W[LX_SLOT(X - 1)];  // rows j+1 (N), j-1 (S)
+  double2& mn = W[LX_SLOT(X + 1)];
+  const double2 nb = mn, sb = W[LX_SLOT(X - 1)];  // rows j+1 (N), j-1 (S)
   const double2 old = m;
   // row kind (row-uniform): 0 interior, 1 bottom ghost, 2 top ghost, 3 keep (halo edge / outside)
   const int rk = !RC ? 0 : (j == 0) ? 1 : (j == x.g.ny + 1) ? 2 : (j > x.rmin && j < x.rmax) ? 0 : 3;
+  const int jb = x.c.inlet_jmax + 1;
+  const int rs = !STEP ? 0 : (j < jb) ? 0 : (j == jb) ? 1 : 2;  // (row-uniform)
+  const bool rowc = STEP && j == jb - 1 && rk == 0;              // the corner's south neighbour's row
+  const int Hh = lc.H0 + X - 1;                                   // this half-sweep
+  const int c0k = x.c.step_i + jb - 1;                            // i + j of the corner's south neighbour
   constexpr bool A = ((JPAR ^ COLOR) & 1) == 0;
   if constexpr (A) {
-    const double nv = lxo_value<CASE, EDGE, RC>(x, rk, cc.ka, m.x, dpp_from_left(m.y), m.y, sb.x, nb.x, fc.x);
+    // the corner's south neighbour (column si in slot a): p_N = the corner of E's new value
+    const bool isc = rowc && cc.sa == 1;
+    const bool first = act.u == 0u;
+    const double cv = ((0.0 + nb.y) + m.x) * 0.5;  // E = (jb, si+1) is slot b of this lane in row jb
+    const double pN = (isc && !first) ? cv : nb.x;
+    const double nv = lxo_value<CASE, EDGE, RC, STEP>(x, rk, cc.ka, rs, cc.sa, m.x, dpp_from_left(m.y), m.y, sb.x,
+                                                      pN, fc.x);
+    bool on = true;
     if constexpr ((MODE & LX_ACT) != 0) {
-      const bool shifted = (RC && rk == 1) || (EDGE && cc.ka == 1);  // left / bottom ghost: two half-sweeps later
-      m.x = (shifted ? act.a2 : act.a) ? nv : m.x;
+      // left / bottom ghost and step-column solid: two half-sweeps later
+      const bool shifted = (RC && rk == 1) || (EDGE && cc.ka == 1) || (STEP && rk == 0 && rs == 2 && cc.sa == 1);
+      on = shifted ? act.a2 : act.a;
+      m.x = on ? nv : m.x;
     } else {
       m.x = nv;
     }
+    if constexpr (STEP) {
+      if (isc && on && !first) mn.x = cv;  // the corner's register (row jb, column si)
+      if constexpr (FULL && RES) {  // the pending residual of the previous iteration (deferred)
+        const bool own = isc && on && x.out_lane && j >= x.y0 && j < x.y1;
+        const int kc = (Hh - c0k) / 2 + 1;  // this update's iteration
+        double xp = d.xp, ps = d.ps;
+        int kd = d.k;
+        if (FIRSTH && own && kd != kc - 1) {  // evaluated in the previous launch's last half-sweep
+          xp = L.cscr[0];
+          ps = L.cscr[1];
+          const double kdd = L.cscr[2];
+          kd = (kdd == kdd) ? (int)kdd : -1;  // (NaN: nothing pending)
+        }
+        if (own && kd == kc - 1 && !first) {
+          const double r = xp + ((cv - 2.0 * old.x) + ps) * x.c.idy2 - fc.x;
+          if (fabs(r) > lc.tol) {
+            const int q = L.kmax + kd;
+            atomicOr(&L.bits[q >> 6], 1ull << (q & 63));
+          }
+        }
+        if (isc) d.k = -1;
+      }
+    }
   } else {  // (column 0 is always slot a)
-    const double nv = lxo_value<CASE, EDGE, RC>(x, rk, cc.kb, m.y, m.x, dpp_from_right(m.x), sb.y, nb.y, fc.y);
-    if constexpr ((MODE & LX_ACT) != 0) m.y = ((RC && rk == 1) ? act.b2 : act.b) ? nv : m.y;
-    else m.y = nv;
+    const bool isc = rowc && cc.sb == 1;
+    const bool first = act.u == 1u;  // slot b: u - 1 == 0
+    const double cv = ((0.0 + dpp_from_right(nb.x)) + m.y) * 0.5;  // E = slot a of lane + 1 in row jb
+    const double pN = (isc && !first) ? cv : nb.y;
+    const double nv = lxo_value<CASE, EDGE, RC, STEP>(x, rk, cc.kb, rs, cc.sb, m.y, m.x, dpp_from_right(m.x), sb.y,
+                                                      pN, fc.y);
+    bool on = true;
+    if constexpr ((MODE & LX_ACT) != 0) {
+      const bool shifted = (RC && rk == 1) || (STEP && rk == 0 && rs == 2 && cc.sb == 1);
+      on = shifted ? act.b2 : act.b;
+      m.y = on ? nv : m.y;
+    } else {
+      m.y = nv;
+    }
+    if constexpr (STEP) {
+      if (isc && on && !first) mn.y = cv;
+      if constexpr (FULL && RES) {
+        const bool own = isc && on && x.out_lane && j >= x.y0 && j < x.y1;
+        const int kc = (Hh - c0k) / 2 + 1;
+        double xp = d.xp, ps = d.ps;
+        int kd = d.k;
+        if (FIRSTH && own && kd != kc - 1) {
+          xp = L.cscr[0];
+          ps = L.cscr[1];
+          const double kdd = L.cscr[2];
+          kd = (kdd == kdd) ? (int)kdd : -1;  // (NaN: nothing pending)
+        }
+        if (own && kd == kc - 1 && !first) {
+          const double r = xp + ((cv - 2.0 * old.y) + ps) * x.c.idy2 - fc.y;
+          if (fabs(r) > lc.tol) {
+            const int q = L.kmax + kd;
+            atomicOr(&L.bits[q >> 6], 1ull << (q & 63));
+          }
+        }
+        if (isc) d.k = -1;
+      }
+    }
   }
   if (STORE && j >= x.y0 && j < x.y1 && x.out_lane) {
     double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
@@ -371,16 +498,57 @@ __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& 
   bool ex;
   if constexpr (A) {  // the other colour at gi+1: W = gi (old; the left ghost when gi+1 == 1), E = gi+2 (new)
     const double pc = m.y;
-    const double pW = (EDGE && x.gi == 0) ? pc : old.x;
+    double pW = (EDGE && x.gi == 0) ? pc : old.x;
+    if constexpr (STEP) pW = (rs == 2 && cc.sa == 1) ? 0.0 + pc : pW;  // W = the step-column solid
     const double pS = row1 ? pc : sb.y;
-    ex = fabs(residual_at<CASE>(x.c, 0, 0, 0, 0, pc, pW, dpp_from_right(m.x), pS, nb.y, fc.y)) > thr;
+    const double pE = dpp_from_right(m.x);
+    ex = fabs(residual_at<CASE>(x.c, 0, 0, 0, 0, pc, pW, pE, pS, nb.y, fc.y)) > thr;
     if constexpr (EDGE) ex = ex && cc.kb == 3;
+    if constexpr (STEP) {
+      ex = ex && (rs == 0 || cc.sb == 2);  // fluid cells only
+      if (rowc && cc.sb == 1) {  // the corner's south neighbour: its p_N is not known yet (deferred)
+        ex = false;
+        bool on = true;
+        if constexpr ((MODE & LX_ACT) != 0) on = act.c;
+        if (FULL && on) {
+          d.xp = (pE - 2.0 * pc + pW) * x.c.idx2;
+          d.ps = pS;
+          d.k = (Hh - 1 - c0k) / 2 + 1;
+          if (LASTH && x.out_lane && rrow) {
+            L.cscr[0] = d.xp;
+            L.cscr[1] = d.ps;
+            L.cscr[2] = (double)d.k;
+          }
+        }
+      }
+    }
     if constexpr ((MODE & LX_ACT) != 0) ex = ex && act.c;
   } else {  // the other colour at gi: W = gi-1 (old; gi is even, never column 1), E = gi+1 (new)
     const double pc = m.x;
+    double pW = dpp_from_left(old.y);
+    if constexpr (STEP) pW = (rs == 2 && cc.sa == 2 && x.gi == x.c.step_i + 1) ? 0.0 + pc : pW;
     const double pS = row1 ? pc : sb.x;
-    ex = fabs(residual_at<CASE>(x.c, 0, 0, 0, 0, pc, dpp_from_left(old.y), m.y, pS, nb.x, fc.x)) > thr;
+    const double pE = m.y;
+    ex = fabs(residual_at<CASE>(x.c, 0, 0, 0, 0, pc, pW, pE, pS, nb.x, fc.x)) > thr;
     if constexpr (EDGE) ex = ex && cc.ka == 3;
+    if constexpr (STEP) {
+      ex = ex && (rs == 0 || cc.sa == 2);
+      if (rowc && cc.sa == 1) {
+        ex = false;
+        bool on = true;
+        if constexpr ((MODE & LX_ACT) != 0) on = act.b;
+        if (FULL && on) {
+          d.xp = (pE - 2.0 * pc + pW) * x.c.idx2;
+          d.ps = pS;
+          d.k = (Hh - 1 - c0k) / 2 + 1;
+          if (LASTH && x.out_lane && rrow) {
+            L.cscr[0] = d.xp;
+            L.cscr[1] = d.ps;
+            L.cscr[2] = (double)d.k;
+          }
+        }
+      }
+    }
     if constexpr ((MODE & LX_ACT) != 0) ex = ex && act.b;
   }
   exi = ex ? 1 : exi;
@@ -395,7 +563,6 @@ __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& 
 // residual row per step for T = 1 .. 2NS, none otherwise). An iteration whose
 // sampled rows all meet the tolerance is left open (LexCtl::kexact, stop
 // code 2) and evaluated exactly by the host (Solver::solve_lexw).
-constexpr int LX_SAMPLE = 2;
 template <int MODE, int T, int X>
 constexpr bool lx_res_row() { return !(MODE & LX_SAMPLE) || T == X; }
 
@@ -407,8 +574,8 @@ struct LxCols {
 };
 
 template <int CASE, int S, int NS, int T, int ROT, int PAR, int MODE, bool EDGE, bool RC>
-__device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCols<CASE>& cl,
-                                          LexRun<NS>& s, int R, const LxAct& act, int& exi) {
+__device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L,
+                                          const LxCols<CASE>& cl, LexRun<NS>& s, int R, const LxAct& act, int& exi) {
   if constexpr (S < NS) {
     // red at R+2S+1 (parity PAR^1) in half-sweep H0+2S; black at R+2S+2 (PAR) in H0+2S+1
     if constexpr (CASE == CAVITY) {
@@ -417,26 +584,26 @@ __device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx
       lx_row<ROT, PAR, 1, MODE, EDGE, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>()>(
           x, lc, cl.cc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi);
     } else {
-      lxo_row<CASE, ROT, PAR ^ 1, 0, MODE, EDGE, RC, false, lx_res_row<MODE, T, 2 * S + 1>()>(
-          x, lc, cl.oc, s.w[S], R + 2 * S + 1, 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi);
-      lxo_row<CASE, ROT, PAR, 1, MODE, EDGE, RC, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>()>(
-          x, lc, cl.oc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi);
+      lxo_row<CASE, ROT, PAR ^ 1, 0, MODE, EDGE, RC, false, lx_res_row<MODE, T, 2 * S + 1>(), S == 0, false>(
+          x, lc, L, cl.oc, s.w[S], R + 2 * S + 1, 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi, s.d);
+      lxo_row<CASE, ROT, PAR, 1, MODE, EDGE, RC, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>(), false, S == NS - 1>(
+          x, lc, L, cl.oc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi, s.d);
     }
     if constexpr (S + 1 < NS) s.w[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
-    lx_sweeps<CASE, S + 1, NS, T, ROT, PAR, MODE, EDGE, RC>(x, lc, cl, s, R, act, exi);
+    lx_sweeps<CASE, S + 1, NS, T, ROT, PAR, MODE, EDGE, RC>(x, lc, L, cl, s, R, act, exi);
   }
 }
 
 template <int CASE, int NS, int T, int ROT, int PAR, int MODE, bool EDGE, bool RC>  // PAR = parity of R, T = step of the unroll
-__device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCols<CASE>& cl,
-                                        LexRun<NS>& s, int R, unsigned long long bit) {
+__device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L,
+                                        const LxCols<CASE>& cl, LexRun<NS>& s, int R, unsigned long long bit) {
   s.w[0][LX_SLOT(0)] = s.np[LX_SLOT(0)];
   s.fr[LX_S10(1)] = s.nf[LX_SLOT(0)];
   s.np[LX_SLOT(-4)] = lx_ld(x, x.pin, R - 4);
   s.nf[LX_SLOT(-4)] = lx_ld(x, x.f, R - 3);
   int exi = 0;
-  const LxAct act = lx_act<MODE>(lc, x.gi, R);
-  lx_sweeps<CASE, 0, NS, T, ROT, PAR, MODE, EDGE, RC>(x, lc, cl, s, R, act, exi);
+  const LxAct act = lx_act<MODE, CASE == BACKSTEP && EDGE && RC>(lc, x.gi, R);
+  lx_sweeps<CASE, 0, NS, T, ROT, PAR, MODE, EDGE, RC>(x, lc, L, cl, s, R, act, exi);
   if constexpr ((MODE & LX_SAMPLE) && (T < 1 || T > 2 * NS)) return;  // (no residual row at this step)
   s.mask |= exi ? bit : 0ull;
 }
@@ -489,23 +656,25 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
     }
   }
   s.mask = 0ull;
+  s.d = LxDefer{0.0, 0.0, -1};
   LxCols<CASE> cl;
   if constexpr (EDGE && CASE == CAVITY) cl.cc[0] = lx_col(x, x.gi), cl.cc[1] = lx_col(x, x.gi + 1);
-  if constexpr (EDGE && CASE != CAVITY) cl.oc = LxoCol{lxo_kind(x, x.gi), lxo_kind(x, x.gi + 1)};
+  if constexpr (EDGE && CASE != CAVITY)
+    cl.oc = LxoCol{lxo_kind(x, x.gi), lxo_kind(x, x.gi + 1), lxs_class(x, x.gi), lxs_class(x, x.gi + 1)};
   int R = Rbeg;
   // (nsteps + 9 <= 127 by the host's band limit: bits t/2 < 64)
 #define LX_BIT(T) ((((st + (T)) >> 1) < 64) ? (1ull << ((st + (T)) >> 1)) : 0ull)
   for (int st = 0; st < nsteps; st += 10, R -= 10) {
-    lx_step<CASE, NS, 0, 0, 0, MODE, EDGE, RC>(x, lc, cl, s, R, LX_BIT(0));
-    lx_step<CASE, NS, 1, 1, 1, MODE, EDGE, RC>(x, lc, cl, s, R - 1, LX_BIT(1));
-    lx_step<CASE, NS, 2, 2, 0, MODE, EDGE, RC>(x, lc, cl, s, R - 2, LX_BIT(2));
-    lx_step<CASE, NS, 3, 3, 1, MODE, EDGE, RC>(x, lc, cl, s, R - 3, LX_BIT(3));
-    lx_step<CASE, NS, 4, 4, 0, MODE, EDGE, RC>(x, lc, cl, s, R - 4, LX_BIT(4));
-    lx_step<CASE, NS, 5, 0, 1, MODE, EDGE, RC>(x, lc, cl, s, R - 5, LX_BIT(5));
-    lx_step<CASE, NS, 6, 1, 0, MODE, EDGE, RC>(x, lc, cl, s, R - 6, LX_BIT(6));
-    lx_step<CASE, NS, 7, 2, 1, MODE, EDGE, RC>(x, lc, cl, s, R - 7, LX_BIT(7));
-    lx_step<CASE, NS, 8, 3, 0, MODE, EDGE, RC>(x, lc, cl, s, R - 8, LX_BIT(8));
-    lx_step<CASE, NS, 9, 4, 1, MODE, EDGE, RC>(x, lc, cl, s, R - 9, LX_BIT(9));
+    lx_step<CASE, NS, 0, 0, 0, MODE, EDGE, RC>(x, lc, L, cl, s, R, LX_BIT(0));
+    lx_step<CASE, NS, 1, 1, 1, MODE, EDGE, RC>(x, lc, L, cl, s, R - 1, LX_BIT(1));
+    lx_step<CASE, NS, 2, 2, 0, MODE, EDGE, RC>(x, lc, L, cl, s, R - 2, LX_BIT(2));
+    lx_step<CASE, NS, 3, 3, 1, MODE, EDGE, RC>(x, lc, L, cl, s, R - 3, LX_BIT(3));
+    lx_step<CASE, NS, 4, 4, 0, MODE, EDGE, RC>(x, lc, L, cl, s, R - 4, LX_BIT(4));
+    lx_step<CASE, NS, 5, 0, 1, MODE, EDGE, RC>(x, lc, L, cl, s, R - 5, LX_BIT(5));
+    lx_step<CASE, NS, 6, 1, 0, MODE, EDGE, RC>(x, lc, L, cl, s, R - 6, LX_BIT(6));
+    lx_step<CASE, NS, 7, 2, 1, MODE, EDGE, RC>(x, lc, L, cl, s, R - 7, LX_BIT(7));
+    lx_step<CASE, NS, 8, 3, 0, MODE, EDGE, RC>(x, lc, L, cl, s, R - 8, LX_BIT(8));
+    lx_step<CASE, NS, 9, 4, 1, MODE, EDGE, RC>(x, lc, L, cl, s, R - 9, LX_BIT(9));
   }
 #undef LX_BIT
   // lane l's bit u <-> iteration Bd0 + u - l = (Bd0 - 63) + (u + 63 - l):
@@ -551,9 +720,9 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
                                                               double* __restrict__ pout, const double* __restrict__ f,
                                                               LexCtl L, int H0, int K, int ka, int kb, PairPlan pl,
                                                               int flags, LexRamp rp) {
-  static_assert(CASE == CAVITY || CASE == CHANNEL, "reference-order march: cavity and channel");
+  static_assert(CASE == CAVITY || CASE == CHANNEL || CASE == BACKSTEP, "reference-order march: case");
   constexpr bool OPEN = CASE != CAVITY;
-  constexpr int CH = 8;  // column halo (lanes 0-3 and 60-63)
+  constexpr int CH = lexw_ch(NS);  // left column halo (lanes 0 .. CH/2-1)
   constexpr int H = 2 * NS + 1;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -660,7 +829,18 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   } else {
     // row checks unless every row the march updates (y0-H+1 .. y1+H+2NS) lies
     // strictly between the stored strip's edge rows (ghost rows included)
-    const bool rc = !(y0 - H + 1 > x.rmin && y1 + H + 2 * NS < x.rmax);
+    bool rc = !(y0 - H + 1 > x.rmin && y1 + H + 2 * NS < x.rmax);
+    bool edge_ = edge;
+    if constexpr (CASE == BACKSTEP) {
+      const int jb = c.inlet_jmax + 1, si = c.step_i;
+      // a march over interior solids only (rows y0-H-1 .. y1+H+2NS+1 in jb+1 ..
+      // ny, columns in 1 .. si-1): nothing it touches ever changes
+      if (c0 >= 1 && c0 + 127 <= si - 1 && y0 - H - 1 >= jb + 1 && y1 + H + 2 * NS + 1 <= g.ny) return;
+      // a march reaching the block (rows >= jb-1, columns <= si+1): the general
+      // tiles (per-cell solid rules, lxo_row STEP)
+      if (y1 + H + 2 * NS + 1 >= jb - 1 && c0 <= si + 1) rc = edge_ = true;
+    }
+    const bool edge = edge_;
     if constexpr (RAMP) {
       const bool full = !rc && smax <= H0 - 2 && Hend <= smin + 2 * (K - 1);
       if (edge) lx_march<CASE, NS, LX_ACT | SM, true, true>(x, lc, L, y0, y1, c0, lane, shard);
@@ -703,6 +883,16 @@ __global__ __launch_bounds__(256) void cavity_resmax_kernel(Geo g, Coef c, const
     m = fmax(gi >= 1 ? ra : 0.0, gi + 1 <= nx ? rb : 0.0);
   }
   block_max_to_shard<256>(m, shards, (blockIdx.y * gridDim.x + blockIdx.x) % RES_SHARDS);
+}
+
+// backwards step, lexicographic order: the corner solid (jb, si) of the final
+// field as the reference's last refresh leaves it, ((0.0 + p_E) + p_S) / 2
+// (backwards_step-01.cpp:708-738; the march keeps the value its south
+// neighbour's last update wrote, one iteration older: lxo_row)
+__global__ void step_corner_kernel(Geo g, Coef c, double* __restrict__ p) {
+  const int jb = c.inlet_jmax + 1, si = c.step_i;
+  if (threadIdx.x != 0 || blockIdx.x != 0 || jb < g.j0 || jb > g.j1) return;
+  p[at(g, jb, si)] = ((0.0 + p[at(g, jb, si + 1)]) + p[at(g, jb - 1, si)]) * 0.5;
 }
 
 // max-norm residual of an open-case field over its fluid cells

@@ -191,11 +191,16 @@ class Solver {
   hipEvent_t ev_f0 = nullptr, ev_f1 = nullptr;
   int resident_lexw_waves = 2048;
   int lexw_edge_pct = 100;  // wall-tile bands as long as interior ones (measured at 4096^2; CFD_LEXW_EDGE_PCT)
-  // the multi-block reference-order march (lexw.hpp): cavity (1-3 sweeps per
-  // launch) and channel (3); the backwards step keeps the one-workgroup kernel
+  // the multi-block reference-order march (lexw.hpp): cavity (1-4 sweeps per
+  // launch), channel and backwards step (4; 3 on strips). The step's solid
+  // rules need a block of at least 2 columns and 2 rows (si >= 2, jb <= ny-1);
+  // other step geometries keep the one-workgroup kernel (poisson_lex_kernel)
+  bool step_lexw_ok() const { return P.step_i >= 2 && P.inlet_jmax >= 1 && P.inlet_jmax <= P.ny - 2; }
   bool use_lexw() const {
-    return P.ordering == CFD_ORDER_LEX && (P.case_id == CFD_CAVITY || P.case_id == CFD_CHANNEL);
+    return P.ordering == CFD_ORDER_LEX &&
+           (P.case_id == CFD_CAVITY || P.case_id == CFD_CHANNEL || (P.case_id == CFD_BACKSTEP && step_lexw_ok()));
   }
+  double* cscr = nullptr;  // the step's deferred corner residual across launches (LexCtl::cscr)
   // sweeps per reference-order launch: 4 (auto) on one strip; strips keep 3
   // (their 8-row halos serve up to 3, lexw.hpp lexw_twc); the cavity also 1-3
   int lexw_ns() const {
@@ -265,6 +270,8 @@ class Solver {
         int lps = 0;
         if (P.case_id == CFD_CHANNEL)
           HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<CHANNEL, 4, false, true>, 256, 0));
+        else if (P.case_id == CFD_BACKSTEP)
+          HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<BACKSTEP, 4, false, true>, 256, 0));
         else if (lexw_ns() == 4)
           HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&lps, poisson_lexw_kernel<CAVITY, 4, false, true>, 256, 0));
         else if (lexw_ns() == 1)
@@ -312,6 +319,7 @@ class Solver {
     HIPC(hipMalloc(&partials, std::max<size_t>(npart, 1) * sizeof(double)));
     HIPC(hipMalloc(&stop, 2 * sizeof(int)));
     HIPC(hipMalloc(&resmax, RES_SHARDS * SHARD_STRIDE * sizeof(double)));
+    HIPC(hipMalloc(&cscr, 4 * sizeof(double)));
     HIPC(hipMemsetAsync(ring, 0, ringn * sizeof(double), st));
     HIPC(hipMemsetAsync(tolv, 0, 4 * sizeof(double), st));
     HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
@@ -396,9 +404,9 @@ class Solver {
       for (auto* p : s.b)
         if (p) (void)hipFree(p);
     S.clear();
-    for (double* p : {ring, srcmax, divmax, tolv, total, partials, resmax})
+    for (double* p : {ring, srcmax, divmax, tolv, total, partials, resmax, cscr})
       if (p) (void)hipFree(p);
-    ring = srcmax = divmax = tolv = total = partials = resmax = nullptr;
+    ring = srcmax = divmax = tolv = total = partials = resmax = cscr = nullptr;
     if (lexbits) (void)hipFree(lexbits);
     lexbits = nullptr;
     lexbits_words = 0;
@@ -432,8 +440,9 @@ class Solver {
     if (!(P.omega > 0) || !(P.omega < 2)) throw Error(CFD_E_ARG, "SOR omega must lie in (0, 2)");
     if (P.max_iters < 0) throw Error(CFD_E_ARG, "max_iters must be >= 0");
     if (P.check_every < 1) throw Error(CFD_E_ARG, "check_every must be >= 1");
-    if (P.sweeps_per_launch < 0 || P.sweeps_per_launch > 4)
-      throw Error(CFD_E_ARG, "sweeps_per_launch must be 0 (auto), 1, 2, 3 or 4");
+    if (P.sweeps_per_launch < 0 || P.sweeps_per_launch > 5 ||
+        (P.sweeps_per_launch == 5 && !(P.ordering == CFD_ORDER_LEX && P.case_id == CFD_CAVITY)))
+      throw Error(CFD_E_ARG, "sweeps_per_launch must be 0 (auto), 1, 2, 3, 4 or 5 (the cavity's lexicographic order)");
     if (P.sweeps_per_launch >= 3 && P.case_id != CFD_CAVITY && P.ordering == CFD_ORDER_RB)
       throw Error(CFD_E_ARG, "three or four red-black sweeps per launch are implemented for the cavity only");
     if (P.sweeps_per_launch >= 1 && P.sweeps_per_launch != 4 && P.ordering == CFD_ORDER_LEX &&
@@ -450,8 +459,9 @@ class Solver {
       throw Error(CFD_E_ARG, "lexicographic ordering runs on one device (strips allowed), not on ranks");
     // (the cavity's lexicographic solve runs on the multi-block wavefront kernel
     // at any size; the open cases on the one-workgroup kernel)
-    if (P.ordering == CFD_ORDER_LEX && P.case_id == CFD_BACKSTEP && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
-      throw Error(CFD_E_ARG, "lexicographic ordering of the backwards step supports nx + ny < 12000");
+    if (P.ordering == CFD_ORDER_LEX && P.case_id == CFD_BACKSTEP && !step_lexw_ok() && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
+      throw Error(CFD_E_ARG, "lexicographic ordering of a backwards step with a block under 2 cells wide or high "
+                             "supports nx + ny < 12000");
     if (P.case_id == CFD_BACKSTEP && (P.step_i <= 0 || P.step_i >= P.nx))
       throw Error(CFD_E_ARG, "Step location is outside computational domain!");
     if (P.case_id == CFD_BACKSTEP && (P.inlet_jmax < 1 || P.inlet_jmax > P.ny))
@@ -922,12 +932,21 @@ class Solver {
 #define CFD_LEXW_LAUNCH(CASE, NS, R, SM) \
   poisson_lexw_kernel<CASE, NS, R, SM><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl, rp)
     // (sampled residual rows: the 3-sweep kernels, the default; 1 and 2 sweeps evaluate every row)
-    if (P.case_id == CFD_CHANNEL && ns == 3) {  // (strips)
+    if (P.case_id == CFD_BACKSTEP && ns == 3) {  // (strips)
+      if (sample) { if (steady) CFD_LEXW_LAUNCH(BACKSTEP, 3, false, true); else CFD_LEXW_LAUNCH(BACKSTEP, 3, true, true); }
+      else { if (steady) CFD_LEXW_LAUNCH(BACKSTEP, 3, false, false); else CFD_LEXW_LAUNCH(BACKSTEP, 3, true, false); }
+    } else if (P.case_id == CFD_BACKSTEP) {
+      if (sample) { if (steady) CFD_LEXW_LAUNCH(BACKSTEP, 4, false, true); else CFD_LEXW_LAUNCH(BACKSTEP, 4, true, true); }
+      else { if (steady) CFD_LEXW_LAUNCH(BACKSTEP, 4, false, false); else CFD_LEXW_LAUNCH(BACKSTEP, 4, true, false); }
+    } else if (P.case_id == CFD_CHANNEL && ns == 3) {  // (strips)
       if (sample) { if (steady) CFD_LEXW_LAUNCH(CHANNEL, 3, false, true); else CFD_LEXW_LAUNCH(CHANNEL, 3, true, true); }
       else { if (steady) CFD_LEXW_LAUNCH(CHANNEL, 3, false, false); else CFD_LEXW_LAUNCH(CHANNEL, 3, true, false); }
     } else if (P.case_id == CFD_CHANNEL) {
       if (sample) { if (steady) CFD_LEXW_LAUNCH(CHANNEL, 4, false, true); else CFD_LEXW_LAUNCH(CHANNEL, 4, true, true); }
       else { if (steady) CFD_LEXW_LAUNCH(CHANNEL, 4, false, false); else CFD_LEXW_LAUNCH(CHANNEL, 4, true, false); }
+    } else if (ns == 5) {
+      if (sample) { if (steady) CFD_LEXW_LAUNCH(CAVITY, 5, false, true); else CFD_LEXW_LAUNCH(CAVITY, 5, true, true); }
+      else { if (steady) CFD_LEXW_LAUNCH(CAVITY, 5, false, false); else CFD_LEXW_LAUNCH(CAVITY, 5, true, false); }
     } else if (ns == 4) {
       if (sample) { if (steady) CFD_LEXW_LAUNCH(CAVITY, 4, false, true); else CFD_LEXW_LAUNCH(CAVITY, 4, true, true); }
       else { if (steady) CFD_LEXW_LAUNCH(CAVITY, 4, false, false); else CFD_LEXW_LAUNCH(CAVITY, 4, true, false); }
@@ -954,7 +973,7 @@ class Solver {
     const int Hlast = P.nx + P.ny + 2 * (K - 1) + (P.case_id != CFD_CAVITY ? 1 : 0);
     const int nl = (Hlast - 2) / (2 * ns) + 1;  // last launch covers Hlast
     const int kmax = lexw_offset();
-    LexCtl L{lexbits, (int)(lexbits_words / LEXW_SHARDS), kmax, tolv, stop, kexact};
+    LexCtl L{lexbits, (int)(lexbits_words / LEXW_SHARDS), kmax, tolv, stop, kexact, cscr};
     // the residual of iteration k of cell (j,i) (half-sweep i+j+2(k-1)) is
     // evaluated in the launch holding half-sweep i+j+2k-1; the corner cell's
     // (i+j = 2) is the first: launches from m_full evaluate iterations >=
@@ -964,7 +983,7 @@ class Solver {
     std::vector<PairPlan> plans(S.size());
     for (size_t q = 0; q < S.size(); ++q)
       plans[q] = multi_plan(S[q].g.wj0, S[q].g.wj1 + 1, 0, 0, resident_lexw_waves / (int)S.size(), ns,
-                            96,  // (a wave's march <= 96 + 19 rows: its iterations fit one 64-bit mask)
+                            ns >= 5 ? 90 : 96,  // (a wave's march steps + 9 <= 127: its iterations fit one 64-bit mask)
                             lexw_edge_pct, lexw_twc(ns), lexw_extra(ns));
     // steady launches: every cell active in every half-sweep of the launch and
     // of the previous one's last (nx+ny+1 <= H0 <= 2K-2NS+1, H0 = 2 + 2NS m)
@@ -1069,6 +1088,16 @@ class Solver {
   void lex_reset_tests() {
     HIPC(hipMemsetAsync(lexbits, 0, lexbits_words * sizeof(unsigned long long), st));
     HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
+    HIPC(hipMemsetAsync(cscr, 0xff, 4 * sizeof(double), st));  // (NaN: no deferred residual pending)
+  }
+  // the step's corner solid of the final field (lexw.hpp step_corner_kernel)
+  void step_corner(int bp) {
+    if (P.case_id != CFD_BACKSTEP) return;
+    if (multi()) exchange(bp, 1);  // (the corner's south neighbour may sit in a halo row)
+    for (auto& s : S) {
+      step_corner_kernel<<<1, 64, 0, st>>>(s.g, C, s.b[bp]);
+      check_launch("step_corner");
+    }
   }
   // replay of k iterations (no tests) from the field in both buffers (base);
   // returns the buffer index (0/1) holding the result
@@ -1127,6 +1156,7 @@ class Solver {
       ++T.proof_fallbacks;
       lex_set_both(-1);
       const int b1 = lex_replay(base, kstop);
+      step_corner(pbuf(b1));  // (also the continuation's initial field: the refresh after iteration kstop)
       const double rk = final_residual(pbuf(b1));
       double t2[2];
       HIPC(hipMemcpy(t2, tolv, sizeof t2, hipMemcpyDeviceToHost));
@@ -1162,6 +1192,7 @@ class Solver {
       HIPC(hipStreamSynchronize(st));
       res = t2[1];
     } else if (res < 0.0) {
+      step_corner(pbuf(fin));
       res = final_residual(pbuf(fin));
     }
     HIPC(hipEventSynchronize(ev_b));

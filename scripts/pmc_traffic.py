@@ -2,7 +2,7 @@
 """FETCH_SIZE / WRITE_SIZE per SOR launch (scripts/pmc_traffic.sh) -> HBM bytes
 per launch with the gfx950 corrections (FETCH_SIZE x2 for 16-B/lane streaming
 reads, WRITE_SIZE exact for 16-B/lane stores: MI355X_MICROARCH.md, HBM
-[CDNA4]). usage: pmc_traffic.py DIR KERNEL_SUBSTRING OUT.json [NX] [SWEEPS_PER_LAUNCH]"""
+[CDNA4]). usage: pmc_traffic.py DIR KERNEL_SUBSTRING OUT.json [NX] [SWEEPS_PER_LAUNCH] [NY]"""
 import csv
 import glob
 import json
@@ -12,6 +12,7 @@ import sys
 d, ksub, out = sys.argv[1], sys.argv[2], sys.argv[3]
 nx = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
 sweeps = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+ny = int(sys.argv[6]) if len(sys.argv) > 6 else nx
 
 
 def per_dispatch(counter):
@@ -30,10 +31,10 @@ wv = sorted(wr.items())
 fv = [x for _, x in fv[len(fv) // 4: 3 * len(fv) // 4]]
 wv = [x for _, x in wv[len(wv) // 4: 3 * len(wv) // 4]]
 fetch_kib, write_kib = statistics.mean(fv), statistics.mean(wv)
-rows = nx + 2
+rows = ny + 2
 alg = 24.0 * rows * (nx + 2)
 rd, wb = 2 * fetch_kib * 1024, write_kib * 1024
-res = {"kernel_match": ksub, "nx": nx, "rows": rows, "sweeps_per_launch": sweeps,
+res = {"kernel_match": ksub, "nx": nx, "ny": ny, "rows": rows, "sweeps_per_launch": sweeps,
        "dispatches": [len(fv), len(wv)], "FETCH_SIZE_KiB_raw": fetch_kib, "WRITE_SIZE_KiB_raw": write_kib,
        "correction": "FETCH_SIZE x2 (gfx950 reports half of 16-B/lane streaming reads), WRITE_SIZE as is "
                      "(exact for 16-B/lane stores): MI355X_MICROARCH.md, HBM [CDNA4]",

@@ -77,10 +77,13 @@ def test_lex_vtk_frame_byte_identical(tmp_path):
     assert hashlib.sha256(fn.read_bytes()).hexdigest() == LOGS["cavity"]["vtk_sha256"]["100"]
 
 
-def test_step_lex_rejects_strips():
-    """The backwards step's reference order runs in one workgroup
-    (poisson_lex_kernel): one strip only. (The cavity's and the channel's run
-    on strips: tests/test_gpu_lexw.py.)"""
+def test_narrow_step_lex_rejects_strips():
+    """A step block one cell wide keeps the one-workgroup reference-order
+    kernel (poisson_lex_kernel): one strip only. (Every other geometry runs
+    the multi-block march on strips: tests/test_gpu_lexw.py.)"""
+    cp = C.make_params("backwards_step", nx=64, ny=32)
+    cp.step_x = 1.5 * cp.dx  # step_i = 1
+    assert cp.step_i == 1
     with pytest.raises(C._lib.CfdError if hasattr(C, "_lib") else Exception):
-        g = C.BackwardsStepSolver(C.reference_defaults("backwards_step"), ordering="lex", n_strips=2)
+        g = C.BackwardsStepSolver(cp, ordering="lex", n_strips=2)
         g.step()

@@ -40,7 +40,7 @@ def random_source(cp, seed=5, scale=10.0):
     return f
 
 
-@pytest.mark.parametrize("spl", [1, 2, 3, 4])
+@pytest.mark.parametrize("spl", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("nx,ny,K", [(40, 24, 37), (300, 130, 25), (129, 257, 1), (129, 257, 2), (257, 64, 113),
                                      (219, 40, 29), (220, 41, 30)])
 def test_capped_solve_bitexact(nx, ny, K, spl):
@@ -61,7 +61,7 @@ def test_capped_solve_strips_bitexact(strips):
     assert_bits(g.field("p"), o.field("p"), f"lexw strips={strips}")
 
 
-@pytest.mark.parametrize("spl", [2, 3, 4])
+@pytest.mark.parametrize("spl", [2, 3, 4, 5])
 def test_converging_solve_stops_at_reference_iteration(spl):
     """The reference's own 63² cavity: a realistic source (one predictor step)
     converges in a few hundred sweeps; the stop is detected up to (nx+ny)/2
@@ -109,10 +109,11 @@ def test_cavity_1024_step_bitexact_capped():
         assert_bits(g.field(name), ofield(o, name, cp), f"1024 {name}")
 
 
-def test_cavity_4096_step_bitexact_capped():
+@pytest.mark.parametrize("spl", [0, 5])
+def test_cavity_4096_step_bitexact_capped(spl):
     """The bench size: one whole timestep in the reference's order (capped)."""
     cp = C.make_params("cavity", re=1000.0, nx=4096, ny=4096, max_iters=24)
-    g = C.CavitySolver(cp, ordering="lex")
+    g = C.CavitySolver(cp, ordering="lex", sweeps_per_launch=spl)
     o = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
     assert g.step() == o.step()
@@ -256,3 +257,86 @@ def test_channel_4096x512_step_bitexact_capped():
         assert g.step() == o.step(), k
     for name in ("u", "v", "p"):
         assert_bits(g.field(name), ofield(o, name, cp), f"channel 4096x512 {name}")
+
+
+# ---- the backwards step (configs[3]) in the reference's order: lexw.hpp STEP ----
+
+def solve_step(cp, f, p0, strips=1, solves=1):
+    g = C.BackwardsStepSolver(cp, ordering="lex", n_strips=strips)
+    o = O.Oracle(cp, ordering=O.LEX)
+    out = []
+    for _ in range(solves):
+        g.set_field("src", f)
+        g.set_field("p", p0)
+        o.field("src")[...] = f
+        o.field("p")[...] = p0
+        out.append((g.solverPressurePoisson(), o.poisson()))
+    return g, o, out
+
+
+@pytest.mark.parametrize("nx,ny,K,strips", [
+    (256, 32, 37, 1),   # step_i 64, jb 17: the corner's south neighbour on an even diagonal (deferral across launches)
+    (260, 34, 41, 1),   # 65, 18 (even diagonal, odd column)
+    (260, 32, 29, 1),   # 65, 17 (odd diagonal)
+    (256, 34, 33, 1),   # 64, 18 (odd diagonal, even column)
+    (436, 32, 26, 1),   # step_i 109: the column after the step opens the second 110-column tile
+    (448, 40, 1, 1), (448, 40, 2, 1), (448, 40, 113, 1),
+    (300, 64, 31, 2), (300, 64, 31, 3),
+])
+def test_step_capped_solve_bitexact(nx, ny, K, strips):
+    """Capped solves (the reference caps at every size): the solid block's
+    refresh in the skew (bottom row, step column, the corner), arbitrary
+    initial solids and ghosts, corner / tile-edge / parity placements, strips."""
+    cp = C.make_params("backwards_step", nx=nx, ny=ny, max_iters=K)
+    f = random_field(cp, 15, 10.0)
+    p0 = random_field(cp, 16)
+    g, o, ((rg, ro),) = solve_step(cp, f, p0, strips)
+    assert rg[0] == ro[0] == K
+    assert rg == ro
+    assert_bits(g.field("p"), o.field("p"), f"step lexw p {nx}x{ny} K={K} strips={strips}")
+
+
+@pytest.mark.parametrize("nx,ny", [(256, 32), (260, 32)])
+def test_step_converging_corner_source_bitexact(nx, ny):
+    """A source spiking at the corner's south neighbour (jb-1, step_i), whose
+    residual is evaluated one half-sweep late (its p_N is the corner refreshed
+    from the east cell's same iteration): converging solves must stop where the
+    reference stops, first with sampled rows (open iterations evaluated
+    exactly), then with every cell evaluated from the hint on (the deferred
+    residual in the full kernels)."""
+    cp = C.make_params("backwards_step", nx=nx, ny=ny, max_iters=5000)
+    f = np.zeros((cp.ny + 2, cp.nx + 2))
+    jb, si = cp.inlet_jmax + 1, cp.step_i
+    f[jb - 1, si] = 40.0
+    f[3, cp.nx - 5] = -25.0
+    f[jb - 2, si + 3] = 7.0
+    g, o, res = solve_step(cp, f, np.zeros_like(f), solves=2)
+    for k, (rg, ro) in enumerate(res):
+        assert 20 < ro[0] < cp.max_iters
+        assert rg == ro, k
+    assert_bits(g.field("p"), o.field("p"), "step converged p")
+
+
+def test_step_reference_run_bitexact():
+    """The reference's own step (256x32) over whole timesteps (the reference
+    hits the 10000-sweep cap here from step 2: 3 steps)."""
+    cp = C.reference_defaults("backwards_step")
+    g = C.BackwardsStepSolver(cp, ordering="lex")
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.velocity_bc(False)
+    for k in range(3):
+        assert g.step() == o.step(), k
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"step reference {name}")
+
+
+def test_step_8192x512_step_bitexact_capped():
+    """BASELINE configs[3] (backwards step Re=400, 8192x512) on one device:
+    a whole timestep in the reference's order, capped, bit for bit."""
+    cp = C.make_params("backwards_step", re=400.0, nx=8192, ny=512, max_iters=24)
+    g = C.BackwardsStepSolver(cp, ordering="lex")
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.velocity_bc(False)
+    assert g.step() == o.step()
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"step 8192x512 {name}")
