@@ -390,7 +390,7 @@ template <int CASE, int ROT, int JPAR, int COLOR, int MODE, bool EDGE, bool RC, 
           bool LASTH>
 __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L, const LxoCol& cc,
                                         double2 (&W)[5], int j, int X, const LxAct& act, const double2& fc, int& exi,
-                                        LxDefer& d) {
+                                        LxDefer& d, double2* nxt = nullptr) {
   // the step's general tiles (block boundary, ghosts): per-cell solid rules
   constexpr bool STEP = CASE == BACKSTEP && EDGE && RC;
   constexpr bool FULL = !(MODE & LX_SAMPLE);
@@ -416,15 +416,27 @@ __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& 
                                                       pN, fc.x);
     bool on = true;
     if constexpr ((MODE & LX_ACT) != 0) {
-      // left / bottom ghost and step-column solid: two half-sweeps later
-      const bool shifted = (RC && rk == 1) || (EDGE && cc.ka == 1) || (STEP && rk == 0 && rs == 2 && cc.sa == 1);
+      // left / bottom ghost and step-column solid: two half-sweeps later. (The
+      // left ghosts of the block's rows copy solids: the bottom-row one is
+      // refreshed after them in the skew like a top ghost, so its ghost keeps
+      // the natural time and copies its previous value, as the reference's
+      // ghost pass, which runs before the solid pass, does; interior solids are
+      // constant either way.)
+      const bool lg = EDGE && cc.ka == 1 && !(STEP && rs != 0);
+      const bool shifted = (RC && rk == 1) || lg || (STEP && rk == 0 && rs == 2 && cc.sa == 1);
       on = shifted ? act.a2 : act.a;
       m.x = on ? nv : m.x;
     } else {
       m.x = nv;
     }
     if constexpr (STEP) {
-      if (isc && on && !first) mn.x = cv;  // the corner's register (row jb, column si)
+      if (isc && on && !first) {  // the corner's register (row jb, column si)
+        mn.x = cv;
+        // in a black half-sweep row jb has already moved on: to the next
+        // sweep's ring (nxt), or, in the last sweep, to p_out
+        if (nxt) nxt->x = cv;
+        if (STORE && j + 1 >= x.y0 && j + 1 < x.y1 && x.out_lane) x.pout[at(x.g, j + 1, x.gi)] = cv;
+      }
       if constexpr (FULL && RES) {  // the pending residual of the previous iteration (deferred)
         const bool own = isc && on && x.out_lane && j >= x.y0 && j < x.y1;
         const int kc = (Hh - c0k) / 2 + 1;  // this update's iteration
@@ -462,7 +474,11 @@ __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& 
       m.y = nv;
     }
     if constexpr (STEP) {
-      if (isc && on && !first) mn.y = cv;
+      if (isc && on && !first) {
+        mn.y = cv;
+        if (nxt) nxt->y = cv;
+        if (STORE && j + 1 >= x.y0 && j + 1 < x.y1 && x.out_lane) x.pout[at(x.g, j + 1, x.gi + 1)] = cv;
+      }
       if constexpr (FULL && RES) {
         const bool own = isc && on && x.out_lane && j >= x.y0 && j < x.y1;
         const int kc = (Hh - c0k) / 2 + 1;
@@ -586,8 +602,10 @@ __device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx
     } else {
       lxo_row<CASE, ROT, PAR ^ 1, 0, MODE, EDGE, RC, false, lx_res_row<MODE, T, 2 * S + 1>(), S == 0, false>(
           x, lc, L, cl.oc, s.w[S], R + 2 * S + 1, 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi, s.d);
+      double2* nxt = nullptr;  // row R+2S+3 in the next sweep's ring (the step's corner write)
+      if constexpr (S + 1 < NS) nxt = &s.w[S + 1][LX_SLOT(2 * S + 3)];
       lxo_row<CASE, ROT, PAR, 1, MODE, EDGE, RC, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>(), false, S == NS - 1>(
-          x, lc, L, cl.oc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi, s.d);
+          x, lc, L, cl.oc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi, s.d, nxt);
     }
     if constexpr (S + 1 < NS) s.w[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
     lx_sweeps<CASE, S + 1, NS, T, ROT, PAR, MODE, EDGE, RC>(x, lc, L, cl, s, R, act, exi);

@@ -305,6 +305,7 @@ def test_step_converging_corner_source_bitexact(nx, ny):
     exactly), then with every cell evaluated from the hint on (the deferred
     residual in the full kernels)."""
     cp = C.make_params("backwards_step", nx=nx, ny=ny, max_iters=5000)
+    cp.tol_factor = 3e-3  # (converges in ~1350 sweeps; the reference's 1e-7 caps here)
     f = np.zeros((cp.ny + 2, cp.nx + 2))
     jb, si = cp.inlet_jmax + 1, cp.step_i
     f[jb - 1, si] = 40.0
