@@ -86,6 +86,45 @@ def cpu_baseline(nx: int, ny: int, budget_s: float, case: str = "cavity") -> dic
                       f"{nx}x{ny} {case} after one predictor step, {el:.1f} s single-threaded"}
 
 
+def reference_binary(timeout_s: float = 60.0) -> dict | None:
+    """The reference's own CPU loop, as compiled from the unmodified reference
+    sources (oracle/build_ref.sh -> oracle/_ref/cavity, g++ -std=c++17 -O2),
+    on this host: its compiled-in case (63x63, Re 1000; the reference takes no
+    arguments), timed from launch until it writes frame 100, i.e. after steps
+    1-100. Their SOR sweep counts (tests/golden/cavity_ref_iters.json, from
+    the oracle pinned to this binary; step 100's checked against the
+    binary's own log) give the cell updates. None when the binary is absent."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    exe = os.path.join(ROOT, "oracle", "_ref", "cavity")
+    fix = os.path.join(ROOT, "tests", "golden", "cavity_ref_iters.json")
+    if not (os.path.exists(exe) and os.path.exists(fix)):
+        return None
+    d = json.load(open(fix))
+    wd = tempfile.mkdtemp(prefix="cfd_ref_")
+    try:
+        t0 = time.perf_counter()
+        proc = subprocess.Popen([exe], cwd=wd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        frame = os.path.join(wd, "vtk_output", "cavity_flow_000100.vtk")
+        while not os.path.exists(frame) and proc.poll() is None and time.perf_counter() - t0 < timeout_s:
+            time.sleep(0.02)
+        el = time.perf_counter() - t0
+        ok = os.path.exists(frame)
+        proc.kill()
+        proc.wait()
+    finally:
+        shutil.rmtree(wd, ignore_errors=True)
+    if not ok:
+        return None
+    sweeps = sum(d["steps"])
+    return {"value": round(d["cells"] * sweeps / el / 1e6, 3), "unit": "MLUPS", "cores": 1, "kind": "reference",
+            "sample": f"the reference binary (cavity-01.cpp, g++ -O2, unmodified) on its compiled-in 63x63 Re=1000 "
+                      f"run, steps 1-100 ({sweeps} SOR sweeps + residuals, predictor, corrector, frame output) "
+                      f"in {el:.2f} s single-threaded"}
+
+
 def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch: int) -> dict:
     """The same workload in the reference's lexicographic sweep order
     (ordering="lex": poisson_lexw_kernel, bit-identical to the reference's
@@ -94,8 +133,7 @@ def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch
     a solve touch part of the grid)."""
     import torch
 
-    s = C.solver_for(cp, device=device, check_every=check_every, ordering="lex",
-                     sweeps_per_launch=args.sweeps_per_launch)
+    s = C.solver_for(cp, device=device, check_every=check_every, ordering="lex", sweeps_per_launch=args.lex_sweeps)
     if args.case == "cavity":
         s.applyBoundaryConditions()
     s.step()  # warmup
@@ -166,6 +204,8 @@ def main() -> int:
                     help="red-black cavity: proof-mode convergence test (off: exact residual every sweep)")
     ap.add_argument("--ordering", default="rb", choices=["rb", "lex"],
                     help="SOR sweep order: rb (red-black) or lex (the reference's lexicographic order, bit-identical)")
+    ap.add_argument("--lex-sweeps", type=int, default=0,
+                    help="reference_order: sweeps per lexicographic-order launch (0: auto = 4; 5 for the cavity)")
     ap.add_argument("--lex-steps", type=int, default=2,
                     help="N=1 cavity: also time this many steps in the reference's own (lexicographic) order "
                          "(0: skip); reported as reference_order")
@@ -325,6 +365,8 @@ def main() -> int:
         if not args.no_cpu_baseline and world == 1:  # the CPU leg is timed at N=1 only
             log("timing the CPU baseline ...")
             line["cpu_baseline"] = cpu_baseline(cp.nx, cp.ny, args.cpu_seconds, args.case)
+            if args.case == "cavity":  # beside it: the reference's own binary on its own case (same host)
+                line["cpu_baseline"]["reference_binary"] = reference_binary()
 
     if (rank == 0 and world == 1 and args.lex_steps > 0 and args.ordering == "rb"
             and kcase_of(args.case) in ("cavity", "channel")):

@@ -1,32 +1,25 @@
 #!/usr/bin/env python3
 """ms per cavity step (Re=100) at reference-like sizes: the one-workgroup solve
-(small.hpp) against the multi-launch solve (CFD_SMALL=0), for choosing the
-crossover (Solver::use_small)."""
+(small.hpp) against the multi-launch solve (small_solve="off"), for choosing
+the crossover (Solver::use_small)."""
 import os
-import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "computational-fluid-dynamics_amd"))
 
-if len(sys.argv) == 1:  # driver: one child per setting (the switch is read at solver creation)
-    for small in ("1", "0"):
-        for n, dt in ((63, 0.0), (96, 0.0), (128, 1e-3)):
-            env = dict(os.environ, CFD_SMALL=small)
-            subprocess.run([sys.executable, __file__, str(n), str(dt)], env=env, check=True)
-    sys.exit(0)
-
 import cfd_amd as C  # noqa: E402
 
-n, dt = int(sys.argv[1]), float(sys.argv[2])
-cp = C.make_params("cavity", re=100.0, nx=n, ny=n, dt=dt if dt > 0 else None)
-s = C.solver_for(cp)
-s.applyBoundaryConditions()
-s.step()
-t0 = time.perf_counter()
-its = [s.step()[0] for _ in range(200)]
-el = time.perf_counter() - t0
-print(f"CFD_SMALL={os.environ.get('CFD_SMALL')} {n}^2 dt={cp.dt:g}: {el / 200 * 1e3:.3f} ms/step, "
-      f"{sum(its) / len(its):.0f} iterations/step", flush=True)
-s.close()
+for small in ("on", "off"):
+    for n, dt in ((63, 0.0), (96, 0.0), (128, 1e-3)):
+        cp = C.make_params("cavity", re=100.0, nx=n, ny=n, dt=dt if dt > 0 else None)
+        s = C.solver_for(cp, small_solve=small)
+        s.applyBoundaryConditions()
+        s.step()
+        t0 = time.perf_counter()
+        its = [s.step()[0] for _ in range(200)]
+        el = time.perf_counter() - t0
+        print(f"small_solve={small} {n}^2 dt={cp.dt:g}: {el / 200 * 1e3:.3f} ms/step, "
+              f"{sum(its) / len(its):.0f} iterations/step", flush=True)
+        s.close()
