@@ -178,6 +178,7 @@ class Solver {
       case CFD_TUNE_PAIR_EDGE_PCT: pair_edge_pct = std::max(10, std::min(100, v)); break;
       case CFD_TUNE_MARCH_MIN_TH: march_min_th = std::max(1, v); break;
       case CFD_TUNE_TENT_TH: tent_th = std::max(4, v); break;
+      case CFD_TUNE_LEXW_RAMP_PCT: lexw_ramp_pct = std::max(0, std::min(100, v)); break;
       default: throw Error(CFD_E_ARG, "unknown tuning knob");
     }
   }
@@ -191,6 +192,7 @@ class Solver {
   hipEvent_t ev_f0 = nullptr, ev_f1 = nullptr;
   int resident_lexw_waves = 2048;
   int lexw_edge_pct = 100;  // wall-tile bands as long as interior ones (measured at 4096^2; CFD_LEXW_EDGE_PCT)
+  int lexw_ramp_pct = 0;    // ramp launches: bands at least this % of the steady plan's (CFD_TUNE_LEXW_RAMP_PCT)
   // the multi-block reference-order march (lexw.hpp): cavity (1-4 sweeps per
   // launch), channel and backwards step (4; 3 on strips). The step's solid
   // rules need a block of at least 2 columns and 2 rows (si >= 2, jb <= ny-1);
@@ -920,6 +922,8 @@ class Solver {
         return n;
       };
       int th = (int)std::max<long long>(1, (tot + waves - 1) / std::max(1, waves));
+      // (a floor on the band height trades idle wave slots for less pipeline fill per output row)
+      th = std::max(th, pl.th * lexw_ramp_pct / 100);
       th = std::max(1, (th + ex + 9) / 10 * 10 - ex);
       while ((rh - rl) / th + 1 > LEXW_RAMP_BANDS) th += 10;
       ntiles = build(th);

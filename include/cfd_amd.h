@@ -195,7 +195,8 @@ enum cfd_tuning {
   CFD_TUNE_LEXW_EDGE_PCT = 3, /* wall-tile band length, % of the interior band (10..100) */
   CFD_TUNE_PAIR_EDGE_PCT = 4, /* boundary-column band length of red-black launches, % (10..100) */
   CFD_TUNE_MARCH_MIN_TH = 5,  /* minimum rows per band of a march launch (>= 1) */
-  CFD_TUNE_TENT_TH = 6        /* rows per band of the predictor's march (>= 4) */
+  CFD_TUNE_TENT_TH = 6,       /* rows per band of the predictor's march (>= 4) */
+  CFD_TUNE_LEXW_RAMP_PCT = 7  /* lexicographic ramp launches: band height floor, % of the steady plan's (0..100) */
 };
 int cfd_set_tuning(cfd_solver* s, int knob, int value);
 

@@ -22,10 +22,12 @@ for case, kw, spls in CASES:
         continue
     cp = C.make_params(case, max_iters=K, **kw)
     for spl in spls:
-        for waves in [int(w) for w in os.environ.get("WAVES", "0,256,512,1024,1536").split(",")]:
+        for waves, rpct in [tuple(int(v) for v in w.split(":")) for w in
+                            os.environ.get("WAVES", "0:0,256:0,512:0,1024:0,1536:0,0:50,0:75,0:100").split(",")]:
             s = C.solver_for(cp, ordering="lex", sweeps_per_launch=spl)
             if waves:
                 s.set_tuning("lexw_waves", waves)
+            s.set_tuning("lexw_ramp_pct", rpct)
             if case == "cavity":
                 s.applyBoundaryConditions()
             s.step()
@@ -37,7 +39,7 @@ for case, kw, spls in CASES:
             el = time.perf_counter() - t0
             tm = s.timing()
             s.close()
-            print(json.dumps({"case": case, "spl": spl, "lexw_waves": waves or "auto", "iters": it,
+            print(json.dumps({"case": case, "spl": spl, "lexw_waves": waves or "auto", "ramp_pct": rpct, "iters": it,
                               "ms_step": round(el * 1e3, 2), "poisson_ms": round(tm.poisson_ms, 2),
                               "launches": tm.poisson_launches,
                               "steady_us": round(tm.poisson_steady_ms / max(tm.poisson_steady_launches, 1) * 1e3, 2),

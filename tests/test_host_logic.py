@@ -72,7 +72,7 @@ def test_switches_default_to_auto_and_map():
     assert (lp.proof_test, lp.small_solve, lp.overlap) == (0, 0, 0)
     cp = C.solver.to_cparams(C.make_params("cavity"), proof_test="off", small_solve="on", overlap="off")
     assert (cp.proof_test, cp.small_solve, cp.overlap) == (2, 1, 2)
-    assert set(_lib.TUNING.values()) == set(range(7))
+    assert set(_lib.TUNING.values()) == set(range(8))
 
 
 @pytest.mark.parametrize("case", ["cavity", "channel", "backwards_step"])
@@ -151,13 +151,15 @@ def test_invalid_params_rejected():
     ("channel", 3, {}, b"cavity only"), ("channel", 4, {}, b"cavity only"),
     ("cavity", 5, {}, b"sweeps_per_launch"), ("cavity", -1, {}, b"sweeps_per_launch"),
     ("cavity", 4, {"proof_test": "off"}, b"proof-mode test"),
-    ("cavity", 4, {"ordering": "lex"}, b"lexicographic-order kernel"),
+    ("cavity", 6, {"ordering": "lex"}, b"sweeps_per_launch"), ("cavity", 5, {}, b"sweeps_per_launch"),
+    ("channel", 3, {"ordering": "lex"}, b"4 sweeps per launch"),
 ])
 def test_sweeps_per_launch_validated_before_device(case, spl, kw, msg):
     """Parameter errors are reported before any device is touched (the checks
     run first in the solver constructor), so they hold on CPU-only hosts too.
     Four sweeps per launch (the default proof-mode plan, stated) are accepted
-    for the red-black cavity with the proof test."""
+    for the red-black cavity with the proof test; five for the cavity's
+    reference-order kernel only."""
     with pytest.raises(_lib.CfdError) as e:
         C.solver_for(C.make_params(case), sweeps_per_launch=spl, **kw)
     assert msg.decode() in str(e.value)
