@@ -69,13 +69,15 @@ typedef struct cfd_params {
   int check_every;      /* residual test every N SOR iterations (1 = reference) */
   int chunk;            /* SOR launches enqueued between host polls (0 = auto) */
   int ordering;         /* CFD_ORDER_RB (red-black, strips/ranks) or CFD_ORDER_LEX (the reference's
-                           sweep order, bit-identical: cavity / Rayleigh-Benard at any size and in
-                           strips on one device; channel / step on one workgroup, nx+ny < 12000) */
+                           sweep order, bit-identical: every case at any size on one device, strips
+                           on that device allowed; a backwards step whose solid block is under 2
+                           cells wide or high runs on one workgroup, nx+ny < 12000) */
   int sweeps_per_launch; /* SOR iterations fused into one kernel launch, bit-identical for every value:
                            0 = auto (red-black cavity: 4 in proof-mode launches, 3 in exact-residual
-                           ones; red-black channel / step: 2; lexicographic cavity: 3);
-                           1, 2; 3 (cavity: every launch 3); 4 (red-black cavity with the proof test:
-                           the auto plan, stated) */
+                           ones; red-black channel / step: 2; lexicographic order: 4, 3 on strips);
+                           1, 2; 3 (cavity: every launch 3); 4 (red-black cavity with the proof test,
+                           or the lexicographic order: the auto plan, stated); 5 (lexicographic
+                           cavity on one strip) */
   /* Rayleigh-Benard (case 3), free-fall units: H = 1, U = sqrt(g beta dT H),
    * nu = sqrt(Pr/Ra), kappa = 1/sqrt(Ra Pr); hot bottom wall t_hot, cold top
    * wall t_cold, adiabatic side walls; buoyancy (T - t_ref) on v. */
