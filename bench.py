@@ -209,6 +209,9 @@ def main() -> int:
     ap.add_argument("--lex-steps", type=int, default=2,
                     help="N=1 cavity: also time this many steps in the reference's own (lexicographic) order "
                          "(0: skip); reported as reference_order")
+    ap.add_argument("--tile-rounds", type=int, default=-1,
+                    help="red-black, one GPU: LDS-tile SOR launches when the grid fits this many resident rounds of "
+                         "tiles (0: never; -1: the library default, 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -237,6 +240,7 @@ def main() -> int:
         cp = C.make_params(args.case, ra=args.ra, nx=args.nx, ny=ny_global, max_iters=args.max_iters)
     else:
         cp = C.make_params(args.case, re=args.re, nx=args.nx, ny=ny_global, max_iters=args.max_iters)
+    tuning = {} if args.tile_rounds < 0 else {"tile_rounds": args.tile_rounds}
     comm = None
     comm_info = None
     if world > 1:
@@ -251,7 +255,7 @@ def main() -> int:
     else:
         solver = C.solver_for(cp, device=local_rank, check_every=check_every,
                               sweeps_per_launch=args.sweeps_per_launch, ordering=args.ordering,
-                              proof_test=args.proof_test)
+                              proof_test=args.proof_test, tuning=tuning)
 
     def barrier():
         if world > 1:
@@ -309,8 +313,10 @@ def main() -> int:
         kcase = kcase_of(args.case)
         # red-black cavity launches: proof-mode convergence test (DESIGN.md
         # §2; --proof-test off evaluates the residual in every sweep)
-        proof = (not lexw and kcase == "cavity" and round(sweeps_per_launch) >= 3
-                 and args.proof_test != "off")
+        sor_kernel = _lib.SOR_KERNEL.get(tm.sor_kernel, "?")
+        proof = (not lexw and args.proof_test != "off"
+                 and (sor_kernel == "tile" or (sor_kernel == "march" and kcase == "cavity"
+                                               and round(sweeps_per_launch) >= 3)))
         rows_here = g1 - g0 + 1
         per_gpu = (f"{cp.nx}x{rows_here} fp64 cells per GPU (global {cp.nx}x{cp.ny} split over {n_gpus} GPUs)"
                    if strong else f"{cp.nx}x{args.ny} fp64 cells per GPU (global {cp.nx}x{cp.ny})")
@@ -351,6 +357,9 @@ def main() -> int:
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel": (f"poisson_lexw_kernel<{kcase},{round(sweeps_per_launch)},sampled> (steady launches)" if lexw
+                           else f"poisson_tile_kernel<{kcase},{'proof' if proof else 'exact'}> "
+                                f"({round(sweeps_per_launch)} sweeps per launch)"
+                           if sor_kernel == "tile"
                            else f"poisson_multi_kernel<{kcase},{round(sweeps_per_launch)},proof>" if proof
                            else f"poisson_multi_kernel<{kcase},3>" if sweeps_per_launch > 2.5
                            else f"poisson_multi_kernel<{kcase},2>" if sweeps_per_launch > 1.5

@@ -13,138 +13,9 @@
 // neighbours on each side.
 #pragma once
 
-#include <hip/hip_runtime.h>
-#include <stdint.h>
+#include "device.hpp"
 
 namespace cfd {
-
-constexpr int CAVITY = 0, CHANNEL = 1, BACKSTEP = 2;
-#ifndef CFD_WAVE_MIN_WAVES
-#define CFD_WAVE_MIN_WAVES 3  // waves per SIMD the SOR wave kernel must fit (4 would cap VGPRs at 128 and spill)
-#endif
-constexpr int HALO = 8;           // halo rows stored per side (a fused pair of SOR iterations needs 7)
-constexpr int RES_SHARDS = 32;    // residual / max accumulators, one 128-B line each
-constexpr int SHARD_STRIDE = 16;  // doubles between shards (128 B)
-constexpr int RING = 16;          // residual ring slots (iteration k uses k & 15)
-// Slots a launch of iterations k..k+NS-1 clears for the next launch: k+NS ..
-// k+NS+RING_AHEAD-1, as many as the longest launch (4 sweeps). The farthest,
-// k+NS+3 = k+NS+3-16 mod RING, lies below every slot still read: the tested
-// window (at most two launches back, >= k-8) and this launch's own.
-constexpr int RING_AHEAD = 4;
-static_assert(4 + RING_AHEAD + 8 <= RING, "ring too small for the tested window and the cleared slots");
-
-struct Geo {
-  int nx, ny;      // global interior cells
-  int pitch;       // doubles per stored row
-  int row_lo;      // global row index of stored row 0
-  int nrows;       // stored rows
-  int j0, j1;      // owned interior rows (global, inclusive)
-  int wj0, wj1;    // owned rows incl. physical ghost rows on boundary strips
-};
-
-struct Coef {
-  int case_id;
-  int step_i, inlet_jmax;  // backwards step: solid block is i <= step_i, j > inlet_jmax
-  double dx, dy;
-  double idx, idy, idx2, idy2;  // 1/dx, 1/dy, 1/(dx*dx), 1/(dy*dy)
-  double nu, dt, rho, u_ref;
-  double omega;
-  double one_m_omega;      // 1.0 - omega (same rounding as the reference's expression)
-  double om_nc[5];         // cavity: omega / neighbour_count for counts 0..4
-  double h2;               // cavity: grid_spacing * grid_spacing
-  double denom;            // open cases: 2*(idx2+idy2)
-  double rdenom;           // open cases: 1.0 / denom (correctly rounded, host)
-  double cav_src;          // cavity: (1/dt) * rho           (cavity-01.cpp:624)
-  double open_src;         // open:   rho / dt               (channel-01.cpp:610)
-  double cav_corr;         // cavity: (dt/h) * rho           (cavity-01.cpp:696,701)
-  double open_cu, open_cv; // open:   dt/(rho*dx), dt/(rho*dy) (channel-01.cpp:697,701)
-  double tol_factor, abs_tol;
-  double proof_k;          // cavity proof-mode test: |K| = 4 idx2 |1-omega| / omega (0: test unavailable)
-  // Rayleigh-Benard (runs as case CAVITY with the lid at rest, plus T)
-  double kappa, buoy, t_hot, t_cold, t_ref;
-};
-
-// Control block for one Poisson solve (device memory).
-struct PoissonCtl {
-  double* ring;        // RING x RES_SHARDS x SHARD_STRIDE residual accumulators
-  const double* tol;   // [0] tolerance, [1] initial residual, [2] max|source| (set by tol_kernel)
-  int* stop;           // [0] converged flag, [1] iteration count at convergence
-  int check_every;
-};
-
-__device__ __forceinline__ size_t at(const Geo& g, int j, int i) {
-  return (size_t)(j - g.row_lo) * (size_t)g.pitch + (size_t)i;
-}
-
-// backwards_step-01.cpp:492-520 (analytic mask: solid block upstream of the
-// step above the inlet channel); cavity / channel: every interior cell fluid.
-__device__ __forceinline__ bool is_fluid(const Coef& c, int nx, int ny, int j, int i) {
-  if (i < 1 || i > nx || j < 1 || j > ny) return false;
-  if (c.case_id != BACKSTEP) return true;
-  return (i > c.step_i) || (j <= c.inlet_jmax);
-}
-
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-  return v;
-}
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-// Block-wide max of non-negative values -> one atomicMax on a shard.
-template <int NT>
-__device__ __forceinline__ void block_max_to_shard(double v, double* shards, int shard) {
-  __shared__ double red[NT / 64];
-  v = wave_max(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double m = red[0];
-#pragma unroll
-    for (int k = 1; k < NT / 64; ++k) m = fmax(m, red[k]);
-    // Non-negative doubles order like their bit patterns.
-    atomicMax(reinterpret_cast<unsigned long long*>(shards + (size_t)shard * SHARD_STRIDE),
-              (unsigned long long)__double_as_longlong(m));
-  }
-}
-
-// Deterministic block sum (fixed butterfly + fixed wave order).
-template <int NT>
-__device__ __forceinline__ double block_sum(double v) {
-  __shared__ double red[NT / 64];
-  v = wave_sum(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  double s = 0.0;
-  if (threadIdx.x == 0) {
-    s = red[0];
-#pragma unroll
-    for (int k = 1; k < NT / 64; ++k) s += red[k];
-  }
-  return s;  // valid in thread 0
-}
-
-// Row neighbours across lanes (wave shifts).
-// bound_ctrl: the lane without a source (0 resp. 63) reads 0, with no
-// zero-initialised destination to merge into (one v_mov_dpp per dword)
-__device__ __forceinline__ double dpp_from_left(double v) {  // lane l receives lane l-1 (wave_shr:1)
-  int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_mov_dpp(lo, 0x138, 0xf, 0xf, true);
-  hi = __builtin_amdgcn_mov_dpp(hi, 0x138, 0xf, 0xf, true);
-  return __hiloint2double(hi, lo);
-}
-__device__ __forceinline__ double dpp_from_right(double v) {  // lane l receives lane l+1 (wave_shl:1)
-  int lo = __double2loint(v), hi = __double2hiint(v);
-  lo = __builtin_amdgcn_mov_dpp(lo, 0x130, 0xf, 0xf, true);
-  hi = __builtin_amdgcn_mov_dpp(hi, 0x130, 0xf, 0xf, true);
-  return __hiloint2double(hi, lo);
-}
 
 // ------------------------------------------------------------------ BCs --
 
@@ -540,127 +411,6 @@ __global__ void tol_kernel(Coef c, const double* __restrict__ srcmax, double* __
   }
 }
 
-// ------------------------------------------------------------- Poisson --
-//
-// Red-black SOR of the reference's pressure equation. Each launch reads p_in
-// and f once and writes p_out once (24 B per cell) for one or several fused
-// iterations (below); p_in / p_out ping-pong, so tiles never read a
-// neighbour's new values and overlapping halos are recomputed redundantly.
-//
-// SOR updates: cavity-01.cpp:643-654 (indicator form), channel-01.cpp:659-666
-// / backwards_step-01.cpp:900-909 (anisotropic form). Residuals:
-// cavity-01.cpp:659-677, channel-01.cpp:672-681, backwards_step-01.cpp:916-930.
-// Ghost / solid refresh after each sweep: channel-01.cpp:531-541,
-// backwards_step-01.cpp:685-740.
-
-// x / denom, correctly rounded, without the divide sequence: q0 = RN(x*y)
-// with y = RN(1/denom), then two FMA corrections q <- RN(q + RN(x - q*denom)*y)
-// (the residual x - q*denom is exact in an FMA). After the first correction
-// q is a faithful quotient (relative error ~2^-105 before rounding), and y has
-// relative error below 2^-53, so by Markstein's theorem the second correction
-// returns RN(x/denom). denom > 0, so the quotient has x's sign (the copysign
-// keeps -0/denom = -0, which the corrections would turn into +0). Finite,
-// normal operands (pressure sums): no over/underflow. Checked against the
-// hardware divide in tests/test_division.py (random and adversarial denominators).
-__device__ __forceinline__ double div_denom(const Coef& c, double x) {
-  const double d = c.denom, y = c.rdenom;
-  double q = x * y;
-  q = fma(fma(-q, d, x), y, q);
-  q = fma(fma(-q, d, x), y, q);
-  return copysign(q, x);
-}
-
-template <int CASE>
-__device__ __forceinline__ double sor_update(const Coef& c, int nx, int ny, int j, int i, double pc, double pW,
-                                             double pE, double pS, double pN, double fc) {
-  if (CASE == CAVITY) {
-    const int ew = (i > 1) ? 1 : 0;
-    const int ee = (i < nx) ? 1 : 0;
-    const int en = (j < ny) ? 1 : 0;
-    const int es = 1;
-    const int nc = ew + ee + en + es;
-    // c.om_nc[nc] == c.omega / nc and c.one_m_omega == 1.0 - c.omega, computed once on the host.
-    // Indicator products without int->double multiplies: 1*x == x and, for
-    // finite x, 0*x == copysign(0, x) — the same bits as the reference's product.
-    const double tE = ee ? pE : copysign(0.0, pE);
-    const double tW = ew ? pW : copysign(0.0, pW);
-    const double tN = en ? pN : copysign(0.0, pN);
-    // selected as values: a run-time index into Coef (or a select of its
-    // addresses, which the optimiser forms from a select of loads) copies the
-    // whole struct to scratch; the empty asm keeps the loaded values opaque
-    double o1 = c.om_nc[1], o2 = c.om_nc[2], o3 = c.om_nc[3], o4 = c.om_nc[4];
-    asm("" : "+s"(o1), "+s"(o2), "+s"(o3), "+s"(o4));
-    const double om = (nc == 4) ? o4 : (nc == 3) ? o3 : (nc == 2) ? o2 : o1;
-    return pc * c.one_m_omega + om * ((tE + tW) + (tN + pS) - fc * c.h2);
-  } else {
-    const double sum = c.idx2 * (pE + pW) + c.idy2 * (pN + pS);
-    const double gs = div_denom(c, sum - fc);  // (sum - fc) / denom
-    return c.one_m_omega * pc + c.omega * gs;
-  }
-}
-
-template <int CASE>
-__device__ __forceinline__ double residual_at(const Coef& c, int nx, int ny, int j, int i, double pc, double pW,
-                                              double pE, double pS, double pN, double fc) {
-  if (CASE == CAVITY) {
-    const int ew = (i > 1) ? 1 : 0, ee = (i < nx) ? 1 : 0, en = (j < ny) ? 1 : 0, es = 1;
-    const double ih2 = c.idx2;
-    return ih2 * (ee * (pE - pc) + ew * (pW - pc) + en * (pN - pc) + es * (pS - pc)) - fc;
-  } else {
-    const double lap = (pE - 2.0 * pc + pW) * c.idx2 + (pN - 2.0 * pc + pS) * c.idy2;
-    return lap - fc;
-  }
-}
-
-template <int CASE>
-__device__ __forceinline__ bool refresh_value(const Coef& c, int nx, int ny, int gj, int gi, double self,
-                                              double pW, double pE, double pS, double pN, double& out) {
-  // channel-01.cpp:531-541, backwards_step-01.cpp:685-740 (pre-refresh neighbour values)
-  if (CASE == CAVITY) return false;
-  const bool jin = gj >= 1 && gj <= ny, iin = gi >= 1 && gi <= nx;
-  if (gi == 0 && jin) { out = pE; return true; }
-  if (gi == nx + 1 && jin) { out = 0.0; return true; }
-  if (gj == 0 && iin) { out = pN; return true; }
-  if (gj == ny + 1 && iin) { out = pS; return true; }
-  if (CASE == BACKSTEP && jin && iin && !is_fluid(c, nx, ny, gj, gi)) {
-    double sum = 0.0;
-    int n = 0;
-    if (gi > 1 && is_fluid(c, nx, ny, gj, gi - 1)) { sum += pW; n++; }
-    if (gi < nx && is_fluid(c, nx, ny, gj, gi + 1)) { sum += pE; n++; }
-    if (gj > 1 && is_fluid(c, nx, ny, gj - 1, gi)) { sum += pS; n++; }
-    if (gj < ny && is_fluid(c, nx, ny, gj + 1, gi)) { sum += pN; n++; }
-    if (n > 0) { out = sum / n; return true; }
-  }
-  (void)self;
-  return false;
-}
-
-// ---------------------------------------------- Poisson, wave march -----
-//
-// One red-black SOR iteration per launch with no LDS and no barriers: every
-// wave is an independent tile of 128 columns (2 per lane, 16-byte loads and
-// stores) marching down a band of rows, and row neighbours across lanes move
-// by DPP wave shifts. 4 columns each side are halo (recomputed), so a wave
-// writes 120 columns. At front row R one step loads p_in(R), f(R-1); updates
-// red at R-1, black at R-2; refreshes ghosts / solids at R-3; computes the
-// residual and stores at R-4. Rows R+1..R+4 of p_in and f are in flight.
-
-// Residual magnitude for the march kernels: as residual_at, but the cavity's
-// 0/1 indicator products are selects. Only |r| is used (max-norm), and
-// 0*x == +-0 adds nothing to a sum with a non-zero term, so |r| is identical.
-template <int CASE>
-__device__ __forceinline__ double residual_abs(const Coef& c, int nx, int ny, int j, int i, double pc, double pW,
-                                               double pE, double pS, double pN, double fc) {
-  if (CASE == CAVITY) {
-    const double tE = (i < nx) ? (pE - pc) : 0.0;
-    const double tW = (i > 1) ? (pW - pc) : 0.0;
-    const double tN = (j < ny) ? (pN - pc) : 0.0;
-    const double tS = pS - pc;
-    return fabs(c.idx2 * (tE + tW + tN + tS) - fc);
-  } else {
-    return fabs(residual_at<CASE>(c, nx, ny, j, i, pc, pW, pE, pS, pN, fc));
-  }
-}
 
 // Every window is a 5-slot ring addressed with compile-time slots and the
 // march is unrolled by 5, so rows never move between registers. Slot of the
@@ -848,46 +598,6 @@ __device__ __forceinline__ double wave_march_ring(const Geo& g, const Coef& c, c
 }
 #undef CFD_SLOT
 
-// Convergence test of the residual recorded for iteration kk (launch-start
-// test of the reference's while condition, cavity-01.cpp:633): true = go on.
-// proof: the slot holds the proof ratio of iteration kk (go on iff > 1)
-__device__ __forceinline__ bool pair_go_on(const PoissonCtl& ctl, int kk, int lane, double tol, bool proof = false) {
-  double prev;
-  if (kk == 0) {
-    prev = ctl.tol[1];
-  } else {
-    const double* slot = ctl.ring + (size_t)(kk & (RING - 1)) * RES_SHARDS * SHARD_STRIDE;
-    prev = (lane < RES_SHARDS) ? slot[lane * SHARD_STRIDE] : 0.0;
-    prev = wave_max(prev);
-    if (proof) return prev > 1.0;
-  }
-  return prev > tol;
-}
-
-// The reference's while condition for the iterations [ka, kb] the host gave
-// this launch (the previous launch's, or with the lagged test the one before;
-// 0 = the initial residual; others only on check_every multiples): the first
-// one that meets the tolerance ends the solve there. Returns false if this
-// launch has nothing to do (stopped now or earlier). All waves agree.
-// proof (the tested launch ran in proof mode): an iteration the proof does not
-// settle ends the proof-mode launches there (stop code 2); the host evaluates
-// it exactly.
-__device__ __forceinline__ bool window_go_on(const PoissonCtl& ctl, int ka, int kb, int lane, bool first_wave,
-                                             bool proof = false) {
-  if (ctl.stop[0] != 0) return false;
-  const double tol = ctl.tol[0];
-  for (int kk = ka; kk <= kb; ++kk) {
-    if (!(kk == 0 || (kk >= 1 && kk % ctl.check_every == 0))) continue;
-    if (!pair_go_on(ctl, kk, lane, tol, proof)) {
-      if (first_wave && lane == 0) {
-        ctl.stop[1] = kk;
-        ctl.stop[0] = (proof && kk > 0) ? 2 : 1;
-      }
-      return false;
-    }
-  }
-  return true;
-}
 
 template <int CASE>
 __global__ __launch_bounds__(256, CFD_WAVE_MIN_WAVES) void poisson_wave_kernel(Geo g, Coef c, const double* __restrict__ pin,
@@ -968,25 +678,6 @@ struct WavePair {
 #define CFD_PAIR_NPR 5
 #endif
 
-// Interior SOR update / residual magnitude: every neighbour is a fluid cell
-// (cavity: all four indicators are 1, so the reference's products are the
-// plain values). Same operations in the same order as sor_update /
-// residual_abs, hence the same bits; no selects.
-template <int CASE>
-__device__ __forceinline__ double sor_interior(const Coef& c, double pc, double pW, double pE, double pS, double pN,
-                                               double fc) {
-  if (CASE == CAVITY) return pc * c.one_m_omega + c.om_nc[4] * ((pE + pW) + (pN + pS) - fc * c.h2);
-  const double sum = c.idx2 * (pE + pW) + c.idy2 * (pN + pS);
-  const double gs = div_denom(c, sum - fc);  // (sum - fc) / denom
-  return c.one_m_omega * pc + c.omega * gs;
-}
-template <int CASE>
-__device__ __forceinline__ double residual_interior(const Coef& c, double pc, double pW, double pE, double pS,
-                                                    double pN, double fc) {
-  if (CASE == CAVITY) return fabs(c.idx2 * ((pE - pc) + (pW - pc) + (pN - pc) + (pS - pc)) - fc);
-  const double lap = (pE - 2.0 * pc + pW) * c.idx2 + (pN - 2.0 * pc + pS) * c.idy2;
-  return fabs(lap - fc);
-}
 
 template <int CASE>
 struct WaveCtx;
@@ -1305,21 +996,6 @@ __device__ __forceinline__ void cav_edge_lanes(WaveCtx<CAVITY>& x) {
   x.om_bt = pick(nb);
 }
 
-// SOR update of a boundary-column wave's cell: sor_update<CAVITY> with the
-// indicators as lane constants (same operands, same order, same bits)
-__device__ __forceinline__ double cav_edge_sor(const Coef& c, bool top, double ce, double cw, double om, double omt,
-                                               double pc, double pW, double pE, double pS, double pN, double fc) {
-  const double tN = top ? pN * 0.0 : pN;  // row-uniform
-  return pc * c.one_m_omega + (top ? omt : om) * ((pE * ce + pW * cw) + (tN + pS) - fc * c.h2);
-}
-
-// |residual| of a boundary-column wave's cell (residual_abs<CAVITY> with the
-// indicator products; +-0 terms leave |r| unchanged)
-__device__ __forceinline__ double cav_edge_res(const Coef& c, bool top, double ce, double cw, double pc, double pW,
-                                               double pE, double pS, double pN, double fc) {
-  const double tN = top ? (pN - pc) * 0.0 : (pN - pc);
-  return fabs(c.idx2 * ((pE - pc) * ce + (pW - pc) * cw + tN + (pS - pc)) - fc);
-}
 
 // red (COLOR 0) / black (COLOR 1) update of row j = R - X d (parity JPAR).
 // PROOF (interior waves): the black update also records |p' - p| x wgt

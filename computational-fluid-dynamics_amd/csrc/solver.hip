@@ -19,6 +19,7 @@
 #include "kernels.hpp"
 #include "lexw.hpp"
 #include "small.hpp"
+#include "tile.hpp"
 
 namespace cfd {
 
@@ -80,9 +81,12 @@ static Coef make_coef(const cfd_params& p) {
   c.abs_tol = p.abs_tol;
   // proof-mode test (kernels.hpp, proof_ratio): its error bound assumes
   // 1 - omega and omega / 4 exact, i.e. 0.5 <= omega <= 2
+  const bool open = p.case_id == CFD_CHANNEL || p.case_id == CFD_BACKSTEP;
   c.proof_k = (p.omega >= 0.5 && p.omega < 2.0 && p.omega != 1.0)
-                  ? 4.0 * c.idx2 * std::fabs(1.0 - p.omega) / p.omega
+                  ? (open ? c.denom : 4.0 * c.idx2) * std::fabs(1.0 - p.omega) / p.omega
                   : 0.0;
+  c.proof_pm = open ? c.denom : c.idx2;
+  c.proof_fd = open ? c.rdenom * (1.0 + 0x1p-50) : c.h2;
   c.kappa = p.kappa;
   c.buoy = p.buoyancy;
   c.t_hot = p.t_hot;
@@ -126,9 +130,26 @@ class Solver {
   // depth-7 pipeline fits the 8-row halos), 2 for the open cases, 1 or 2 on
   // request (proof-mode launches: proof_ns)
   int sweeps_per_launch() const {
+    if (tile_on) {  // LDS-tile launches: any count up to what the halo covers
+      const int mx = tile_max_sweeps(P.case_id);
+      return (P.sweeps_per_launch >= 1 && P.sweeps_per_launch < mx) ? P.sweeps_per_launch : mx;
+    }
     if (P.sweeps_per_launch == 1) return 1;
     if (P.sweeps_per_launch == 2) return 2;
     return P.case_id == CFD_CAVITY ? 3 : 2;
+  }
+  // LDS-tile launches (tile.hpp): red-black, one strip, no ranks, a grid of at
+  // most tile_rounds resident rounds of tiles (CFD_TUNE_TILE_ROUNDS)
+  bool tile_on = false;
+  int tile_rounds = 1;
+  TilePlan tplan{};
+  void plan_tiles() {
+    tile_on = false;
+    tplan = TilePlan{};
+    if (P.ordering != CFD_ORDER_RB || S.size() != 1 || comm || tile_rounds <= 0) return;
+    const Geo& g = S[0].g;
+    tplan = tile_plan(P.nx, g.wj0, g.wj1 + 1, tile_rounds * n_cu);
+    tile_on = tplan.ctiles > 0;
   }
   struct LaunchRec {
     int first, n;        // iterations first .. first+n-1
@@ -144,6 +165,7 @@ class Solver {
   int proof_ns = 4;           // sweeps per proof-mode launch (4; 3 with sweeps_per_launch = 3)
   bool proof_ok() const {
     // (only interior column tiles prove: at least one between the two boundary tiles)
+    if (tile_on) return proof_enabled && C.proof_k > 0.0;  // tile launches: every case (tile.hip)
     return proof_enabled && P.case_id == CFD_CAVITY && sweeps_per_launch() == 3 && C.proof_k > 0.0 &&
            (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC >= 3;
   }
@@ -179,6 +201,10 @@ class Solver {
       case CFD_TUNE_MARCH_MIN_TH: march_min_th = std::max(1, v); break;
       case CFD_TUNE_TENT_TH: tent_th = std::max(4, v); break;
       case CFD_TUNE_LEXW_RAMP_PCT: lexw_ramp_pct = std::max(0, std::min(100, v)); break;
+      case CFD_TUNE_TILE_ROUNDS:
+        tile_rounds = std::max(0, std::min(v, 16));
+        plan_tiles();
+        break;
       default: throw Error(CFD_E_ARG, "unknown tuning knob");
     }
   }
@@ -346,6 +372,7 @@ class Solver {
         HIPC(hipEventCreateWithFlags(&ev_sync, hipEventDisableTiming));
       }
     }
+    plan_tiles();
     // fluid cells (backwards_step-01.cpp:522-528)
     long long solid = 0;
     if (P.case_id == CFD_BACKSTEP)
@@ -703,6 +730,12 @@ class Solver {
   template <int CASE>
   void launch_poisson(const double* const* pin, double* const* pout, int k, int n, int ka, int kb, bool replay) {
     PoissonCtl ctl{ring, tolv, stop, P.check_every};
+    if (tile_on) {  // one strip (plan_tiles)
+      tile_launch(P.case_id, proof_launch && !replay, S[0].g, C, pin[0], pout[0], S[0].b[B_F], ctl, k, ka, kb, n,
+                  tplan, march_flags | (replay ? 4 : 0) | (window_proof ? 128 : 0), st);
+      check_launch("poisson (tile)");
+      return;
+    }
     for (size_t q = 0; q < S.size(); ++q) {
       const Geo& g = S[q].g;
       const int rows = g.wj1 - g.wj0 + 1;
@@ -1291,17 +1324,21 @@ class Solver {
 
   void solve(cfd_step_info* out) {
     if (use_lexw()) {
+      T.sor_kernel = CFD_SOR_LEXW;
       solve_lexw(out);
       return;
     }
     if (P.ordering == CFD_ORDER_LEX) {
+      T.sor_kernel = CFD_SOR_LEX;
       solve_lex(out);
       return;
     }
     if (use_small()) {
+      T.sor_kernel = CFD_SOR_SMALL;
       solve_small(out);
       return;
     }
+    T.sor_kernel = tile_on ? CFD_SOR_TILE : CFD_SOR_MARCH;
     const int base = pcur;
     HIPC(hipMemsetAsync(ring, 0, (size_t)RING * RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
     HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
@@ -1343,7 +1380,7 @@ class Solver {
       while (k < P.max_iters && !stopped) {
         for (int j = 0; j < chunk && k < P.max_iters; ++j, ++m) {
           const bool proof = m >= proof_from;
-          const int n = std::min(proof ? proof_ns : spl, P.max_iters - k);
+          const int n = std::min((proof && !tile_on) ? proof_ns : spl, P.max_iters - k);  // (tiles: spl either way)
           const int src = m - 1 - lag;
           int ka = 1, kb = 0;  // empty window
           window_proof = false;
@@ -1354,7 +1391,7 @@ class Solver {
           } else if (src == -1) {
             ka = kb = 0;
           }
-          proof_launch = proof && n >= 3;
+          proof_launch = proof && (n >= 3 || tile_on);
           poisson_launch(m, k + 1, n, base, ka, kb, false);
           if (ka <= kb) last_tested = std::max(last_tested, kb);
           launches.push_back({k + 1, n, proof_launch});

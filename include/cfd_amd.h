@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 7
+#define CFD_AMD_ABI_VERSION 8
 
 /* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
  * tree (only figures): it is the cavity's projection step with a resting lid
@@ -121,7 +121,19 @@ typedef struct cfd_timing {
   long long poisson_steady_launches; /* (the ramps at the start / end of a solve excluded) */
   long long proof_fallbacks;  /* red-black cavity: solves whose proof-mode convergence test left an
                                  iteration open, finished with exact residuals */
+  int sor_kernel;             /* enum cfd_sor_kernel: the SOR kernel family of the last solve (ABI 8) */
 } cfd_timing;
+
+/* Which SOR kernel family ran a solve (cfd_timing.sor_kernel); every one gives the same bits for
+ * the same ordering. */
+enum cfd_sor_kernel {
+  CFD_SOR_NONE = 0,
+  CFD_SOR_MARCH = 1,  /* red-black wave-march launches (kernels.hpp), any size, strips and ranks */
+  CFD_SOR_TILE = 2,   /* red-black LDS-tile launches (tile.hpp): one strip of up to ~4 M cells */
+  CFD_SOR_SMALL = 3,  /* red-black whole solve in one workgroup (small.hpp): reference-sized grids */
+  CFD_SOR_LEXW = 4,   /* reference order, multi-block march (lexw.hpp) */
+  CFD_SOR_LEX = 5     /* reference order, one workgroup (poisson_lex_kernel) */
+};
 
 /* Library / ABI info. */
 int cfd_abi_version(void);
@@ -198,7 +210,9 @@ enum cfd_tuning {
   CFD_TUNE_PAIR_EDGE_PCT = 4, /* boundary-column band length of red-black launches, % (10..100) */
   CFD_TUNE_MARCH_MIN_TH = 5,  /* minimum rows per band of a march launch (>= 1) */
   CFD_TUNE_TENT_TH = 6,       /* rows per band of the predictor's march (>= 4) */
-  CFD_TUNE_LEXW_RAMP_PCT = 7  /* lexicographic ramp launches: band height floor, % of the steady plan's (0..100) */
+  CFD_TUNE_LEXW_RAMP_PCT = 7, /* lexicographic ramp launches: band height floor, % of the steady plan's (0..100) */
+  CFD_TUNE_TILE_ROUNDS = 8    /* red-black, one strip: LDS-tile launches when the grid fits this many
+                                 resident rounds of tiles (one per CU; 0: never, the march launches) */
 };
 int cfd_set_tuning(cfd_solver* s, int knob, int value);
 

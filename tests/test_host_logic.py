@@ -44,7 +44,7 @@ def test_nm_exports_match_header():
 
 
 def test_abi_version():
-    assert _lib.lib().cfd_abi_version() == 7
+    assert _lib.lib().cfd_abi_version() == 8
 
 
 def test_params_struct_layout_matches_header(tmp_path):
@@ -65,6 +65,26 @@ def test_params_struct_layout_matches_header(tmp_path):
     assert out[1 + len(fields)].split() == [str(_lib.SWITCH[n]) for n in ("auto", "on", "off")]
 
 
+def test_timing_struct_layout_and_kernel_enum(tmp_path):
+    """The ctypes mirror of cfd_timing matches the C struct (ABI 8 appended
+    sor_kernel), and _lib.SOR_KERNEL names enum cfd_sor_kernel's values."""
+    fields = [f for f, _ in _lib.Timing._fields_]
+    names = ["CFD_SOR_NONE", "CFD_SOR_MARCH", "CFD_SOR_TILE", "CFD_SOR_SMALL", "CFD_SOR_LEXW", "CFD_SOR_LEX"]
+    src = tmp_path / "timing.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "cfd_amd.h"\nint main(void){\n'
+                   '  printf("%zu\\n", sizeof(cfd_timing));\n'
+                   + "".join(f'  printf("%zu\\n", offsetof(cfd_timing, {f}));\n' for f in fields)
+                   + "".join(f'  printf("%d\\n", {n});\n' for n in names) + '  return 0;\n}\n')
+    exe = tmp_path / "timing"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+    assert int(out[0]) == ctypes.sizeof(_lib.Timing)
+    for k, f in enumerate(fields):
+        assert int(out[1 + k]) == getattr(_lib.Timing, f).offset, f
+    vals = [int(x) for x in out[1 + len(fields):]]
+    assert [_lib.SOR_KERNEL[v] for v in vals] == ["none", "march", "tile", "small", "lexw", "lex"]
+
+
 def test_switches_default_to_auto_and_map():
     """cfd_params_init leaves the ABI-7 switches at CFD_AUTO; the Python
     mirror passes "auto" / "on" / "off" through unchanged."""
@@ -72,7 +92,7 @@ def test_switches_default_to_auto_and_map():
     assert (lp.proof_test, lp.small_solve, lp.overlap) == (0, 0, 0)
     cp = C.solver.to_cparams(C.make_params("cavity"), proof_test="off", small_solve="on", overlap="off")
     assert (cp.proof_test, cp.small_solve, cp.overlap) == (2, 1, 2)
-    assert set(_lib.TUNING.values()) == set(range(8))
+    assert set(_lib.TUNING.values()) == set(range(9))
 
 
 @pytest.mark.parametrize("case", ["cavity", "channel", "backwards_step"])
