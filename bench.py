@@ -212,6 +212,8 @@ def main() -> int:
     ap.add_argument("--tile-rounds", type=int, default=-1,
                     help="red-black, one GPU: LDS-tile SOR launches when the grid fits this many resident rounds of "
                          "tiles (0: never; -1: the library default, 1)")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
+                    help="launch-planning knob (cfd_amd._lib.TUNING names; performance only, same bits)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -241,6 +243,9 @@ def main() -> int:
     else:
         cp = C.make_params(args.case, re=args.re, nx=args.nx, ny=ny_global, max_iters=args.max_iters)
     tuning = {} if args.tile_rounds < 0 else {"tile_rounds": args.tile_rounds}
+    for kv in args.tune:
+        k_, v_ = kv.split("=", 1)
+        tuning[k_] = int(v_)
     comm = None
     comm_info = None
     if world > 1:
@@ -315,8 +320,7 @@ def main() -> int:
         # §2; --proof-test off evaluates the residual in every sweep)
         sor_kernel = _lib.SOR_KERNEL.get(tm.sor_kernel, "?")
         proof = (not lexw and args.proof_test != "off"
-                 and (sor_kernel == "tile" or (sor_kernel == "march" and kcase == "cavity"
-                                               and round(sweeps_per_launch) >= 3)))
+                 and (sor_kernel == "tile" or (sor_kernel == "march" and round(sweeps_per_launch) >= 3)))
         rows_here = g1 - g0 + 1
         per_gpu = (f"{cp.nx}x{rows_here} fp64 cells per GPU (global {cp.nx}x{cp.ny} split over {n_gpus} GPUs)"
                    if strong else f"{cp.nx}x{args.ny} fp64 cells per GPU (global {cp.nx}x{cp.ny})")
@@ -360,7 +364,8 @@ def main() -> int:
                            else f"poisson_tile_kernel<{kcase},{'proof' if proof else 'exact'}> "
                                 f"({round(sweeps_per_launch)} sweeps per launch)"
                            if sor_kernel == "tile"
-                           else f"poisson_multi_kernel<{kcase},{round(sweeps_per_launch)},proof>" if proof
+                           else f"poisson_multi_kernel<{kcase},{round(sweeps_per_launch)},proof>" if proof and kcase == "cavity"
+                           else f"poisson_open_proof_kernel<{kcase},{round(sweeps_per_launch)}>" if proof
                            else f"poisson_multi_kernel<{kcase},3>" if sweeps_per_launch > 2.5
                            else f"poisson_multi_kernel<{kcase},2>" if sweeps_per_launch > 1.5
                            else f"poisson_wave_kernel<{kcase}>"),

@@ -345,4 +345,29 @@ __device__ __forceinline__ double cav_edge_res(const Coef& c, bool top, double c
   return fabs(c.idx2 * ((pE - pc) * ce + (pW - pc) * cw + tN + (pS - pc)) - fc);
 }
 
+// Proof-mode ratio of one sweep (march.hpp proof_ratio is
+// the cavity march's form of the same bound; tile.hip and open.hip use this one). A black cell with four
+// neighbours that the sweep's refresh leaves alone has residual
+//   r = K (p' - p) + E,   K = d (1 - w) / w,
+// d = 4 idx2 (cavity: p' = (1-w) p + (w/4)(S - h^2 f), r = idx2 (S - 4 p') - f)
+// or d = 2 (idx2 + idy2) (open cases: p' = (1-w) p + w (S - f) / d,
+// r = S - d p' - f, S = idx2 (pE + pW) + idy2 (pN + pS)). The rounding of the
+// update (five operations and the correctly rounded divide) and of the
+// reference's own evaluation of r stays below 64 u (d P + F) (u = 2^-53, P a
+// bound on every |p| the cell's stencils see, F on |f|); the margin used is
+// 2^-43 (pm P + F) with pm = idx2 (cavity: the march's constant, 8x its bound)
+// or d (16x). A sweep maps P + fd F to at most 9 (P + fd F) (red: |p'| <= 3P
+// + 2 fd F, black from those), fd = h^2 (cavity) or 1/d: P <= 9^nsw (Pin + fd F).
+// |p' - p| > thr = (tol + margin) / |K| (x (1 + 2^-38)) then proves that the
+// reference's computed |r| > tol: its loop goes on. Returns max|p' - p| / thr.
+__device__ __forceinline__ double proof_ratio_gen(const Coef& c, double tol, double dmax, double pin, double fmx,
+                                                   double growth) {
+  const double P = growth * (pin + c.proof_fd * fmx) * (1.0 + 0x1p-40);
+  const double margin = 0x1p-43 * (c.proof_pm * P + fmx);
+  const double thr = (tol + margin) / c.proof_k * (1.0 + 0x1p-38);
+  const double q = dmax / thr;
+  return (q == q && q >= 0.0) ? q : 0.0;  // non-finite bounds prove nothing
+}
+
+
 }  // namespace cfd

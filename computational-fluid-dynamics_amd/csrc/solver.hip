@@ -20,6 +20,7 @@
 #include "lexw.hpp"
 #include "small.hpp"
 #include "tile.hpp"
+#include "open.hpp"
 
 namespace cfd {
 
@@ -166,7 +167,11 @@ class Solver {
   bool proof_ok() const {
     // (only interior column tiles prove: at least one between the two boundary tiles)
     if (tile_on) return proof_enabled && C.proof_k > 0.0;  // tile launches: every case (tile.hip)
-    return proof_enabled && P.case_id == CFD_CAVITY && sweeps_per_launch() == 3 && C.proof_k > 0.0 &&
+    // march launches: the cavity's 3-sweep plan or the open cases' pairs
+    // become 4-sweep proof launches (open cases: open.hip)
+    const bool plan = P.case_id == CFD_CAVITY ? sweeps_per_launch() == 3
+                                              : (P.sweeps_per_launch == 0 || P.sweeps_per_launch == 4);
+    return proof_enabled && plan && C.proof_k > 0.0 &&
            (P.nx + 2 + PAIR_TWC - 1) / PAIR_TWC >= 3;
   }
   std::vector<LaunchRec> launches;  // SOR launches of the current solve
@@ -373,6 +378,9 @@ class Solver {
       }
     }
     plan_tiles();
+    // the step's proof launches on strips / ranks: 3 sweeps (open.hip: its
+    // block edge reads one row deeper than the 4-sweep pipeline's 8)
+    if (P.case_id == CFD_BACKSTEP && multi()) proof_ns = 3;
     // fluid cells (backwards_step-01.cpp:522-528)
     long long solid = 0;
     if (P.case_id == CFD_BACKSTEP)
@@ -472,8 +480,8 @@ class Solver {
     if (P.sweeps_per_launch < 0 || P.sweeps_per_launch > 5 ||
         (P.sweeps_per_launch == 5 && !(P.ordering == CFD_ORDER_LEX && P.case_id == CFD_CAVITY)))
       throw Error(CFD_E_ARG, "sweeps_per_launch must be 0 (auto), 1, 2, 3, 4 or 5 (the cavity's lexicographic order)");
-    if (P.sweeps_per_launch >= 3 && P.case_id != CFD_CAVITY && P.ordering == CFD_ORDER_RB)
-      throw Error(CFD_E_ARG, "three or four red-black sweeps per launch are implemented for the cavity only");
+    if (P.sweeps_per_launch == 3 && P.case_id != CFD_CAVITY && P.ordering == CFD_ORDER_RB)
+      throw Error(CFD_E_ARG, "three red-black sweeps per launch are implemented for the cavity only");
     if (P.sweeps_per_launch >= 1 && P.sweeps_per_launch != 4 && P.ordering == CFD_ORDER_LEX &&
         P.case_id != CFD_CAVITY && P.case_id != CFD_RAYLEIGH_BENARD)
       throw Error(CFD_E_ARG, "the open cases' lexicographic-order kernel runs 4 sweeps per launch (0: auto)");
@@ -642,7 +650,7 @@ class Solver {
   // Rows one interior wave marches beyond its band (both sides together, plus
   // the parity alignment row) for an n-sweep launch: the cavity's pipeline has
   // depth 2n+1, the open cases' pair pipeline 7.
-  int march_extra(int n) const { return (P.case_id == CFD_CAVITY) ? 2 * (2 * n + 1) + 1 : 15; }
+  int march_extra(int n) const { return (P.case_id == CFD_CAVITY || n == 4) ? 2 * (2 * n + 1) + 1 : 15; }
 
   // Tiling of an n-sweep launch over rows [lo0, hi0) + [lo1, hi1) with at most
   // `waves` waves (one resident round). Interior column tiles: bands of th
@@ -720,6 +728,13 @@ class Solver {
           poisson_multi_kernel<CASE, 3, true><<<grid, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, ka, kb, pl, fl);
         else
           poisson_multi_kernel<CASE, 3><<<grid, 256, 0, stream>>>(g, C, pin, pout, f, ctl, k, ka, kb, pl, fl);
+        return;
+      }
+    }
+    if constexpr (CASE != CAVITY) {
+      if (n >= 3) {  // proof mode only (open.hip)
+        if (!proof_launch || replay) throw Error(CFD_E_STATE, "three or four sweeps per launch: proof mode only");
+        open_proof_launch(CASE, n, g, C, pin, pout, f, ctl, k, ka, kb, pl, fl, stream);
         return;
       }
     }
