@@ -168,7 +168,7 @@ def test_invalid_params_rejected():
 
 
 @pytest.mark.parametrize("case,spl,kw,msg", [
-    ("channel", 3, {}, b"cavity only"), ("channel", 4, {}, b"cavity only"),
+    ("channel", 3, {}, b"cavity only"), ("channel", 4, {"proof_test": "off"}, b"proof-mode test"),
     ("cavity", 5, {}, b"sweeps_per_launch"), ("cavity", -1, {}, b"sweeps_per_launch"),
     ("cavity", 4, {"proof_test": "off"}, b"proof-mode test"),
     ("cavity", 6, {"ordering": "lex"}, b"sweeps_per_launch"), ("cavity", 5, {}, b"sweeps_per_launch"),
@@ -178,8 +178,9 @@ def test_sweeps_per_launch_validated_before_device(case, spl, kw, msg):
     """Parameter errors are reported before any device is touched (the checks
     run first in the solver constructor), so they hold on CPU-only hosts too.
     Four sweeps per launch (the default proof-mode plan, stated) are accepted
-    for the red-black cavity with the proof test; five for the cavity's
-    reference-order kernel only."""
+    in red-black order with the proof test (every case since the open cases'
+    proof launches, open.hip); five for the cavity's reference-order kernel
+    only."""
     with pytest.raises(_lib.CfdError) as e:
         C.solver_for(C.make_params(case), sweeps_per_launch=spl, **kw)
     assert msg.decode() in str(e.value)
