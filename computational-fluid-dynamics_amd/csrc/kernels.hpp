@@ -110,13 +110,19 @@ __global__ void bc_step_faces_kernel(Geo g, Coef c, double* __restrict__ u, doub
 // 16-byte loads) and walks down a band of `th` rows keeping rows j-1, j, j+1
 // of u and v in registers; column neighbours move between lanes by DPP. Each
 // row costs one load of u and of v and the stores of u*, v* (32 B per cell plus
-// 2 halo rows per band and 2 halo columns per 128). Output columns: the
-// wave's columns 1..126 (TENT_TWC per tile). Same expressions in the same
+// 2 halo rows per band and 2 halo columns per 128). Output columns: 112 per
+// wave, on 128-B lines (CFD_TENT_ALIGN, below). Same expressions in the same
 // order as the reference loops, hence the same bits.
 #ifndef CFD_TENT_ALIGN
-#define CFD_TENT_ALIGN 1  // 1: tiles of 112 output columns starting on 128-B lines (lanes 4..59 store)
+// 1: tiles of 112 output columns starting on 128-B lines (lanes 4..59 store)
+// 2: tiles of 128 output columns on 1-KB lines, every lane stores; the two
+//    neighbour columns outside the tile come from one extra 8-byte load per
+//    field and row (lane 0: column gi-1, lane 63: column gi+2) - measured
+//    123 us at 4096^2 against 119.5 for 1 (the halo columns were L2 hits)
+// 0: 126 output columns (lanes 1..63 / 0..62)
+#define CFD_TENT_ALIGN 1
 #endif
-constexpr int TENT_TWC = CFD_TENT_ALIGN ? 112 : 126;
+constexpr int TENT_TWC = CFD_TENT_ALIGN == 2 ? 128 : CFD_TENT_ALIGN ? 112 : 126;
 #ifndef CFD_TENT_PD
 #define CFD_TENT_PD 3  // rows of u and v in flight ahead of row j+1
 #endif
@@ -134,15 +140,16 @@ __global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const dou
   const int nx = g.nx, ny = g.ny;
   const bool step = c.case_id == BACKSTEP;
   // this lane's columns gi (a), gi + 1 (b)
-  const int gi = CFD_TENT_ALIGN ? ctile * TENT_TWC - 8 + 2 * lane : ctile * TENT_TWC + 2 * lane;
+  const int gi = CFD_TENT_ALIGN == 1 ? ctile * TENT_TWC - 8 + 2 * lane : ctile * TENT_TWC + 2 * lane;
   const int gic = max(min(gi, g.pitch - 2), 0);     // (lanes past the row read a valid pair)
   const size_t P = (size_t)g.pitch;
   auto ld = [&](const double* base, int j) {
     return *reinterpret_cast<const double2*>(base + (size_t)(j - g.row_lo) * P + gic);
   };
   // output cells: a of lanes 1..63, b of lanes 0..62 (their row neighbours are in the wave)
-  const bool out_a = (CFD_TENT_ALIGN ? lane >= 4 && lane <= 59 : lane >= 1) && gi <= nx;
-  const bool out_b = (CFD_TENT_ALIGN ? lane >= 4 && lane <= 59 : lane <= 62) && gi + 1 <= nx;
+  constexpr bool EDGEL = CFD_TENT_ALIGN == 2;
+  const bool out_a = (EDGEL || (CFD_TENT_ALIGN ? lane >= 4 && lane <= 59 : lane >= 1)) && gi <= nx;
+  const bool out_b = (EDGEL || (CFD_TENT_ALIGN ? lane >= 4 && lane <= 59 : lane <= 62)) && gi + 1 <= nx;
   // rows j+1 .. j+3 of u and v in flight (clamped to the strip's stored rows:
   // rows past y1 are never consumed)
   const int rlast = g.row_lo + g.nrows - 1;
@@ -155,6 +162,21 @@ __global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const dou
     uq[q] = ldc(u, y0 + 1 + q);
     vq[q] = ldc(v, y0 + 1 + q);
   }
+  // EDGEL: the column outside the tile next to lane 0 (gi - 1) / lane 63
+  // (gi + 2); the other lanes read their own column (a line they load anyway)
+  const int ge = EDGEL ? min(max(lane == 0 ? gi - 1 : lane == 63 ? gi + 2 : gi, 0), g.pitch - 1) : 0;
+  auto lde = [&](const double* base, int j) { return base[(size_t)(min(j, rlast) - g.row_lo) * P + ge]; };
+  double ue_c = 0.0, ve_m = 0.0, ve_c = 0.0, ueq[PD], veq[PD];
+  if (EDGEL) {
+    ue_c = lde(u, y0);
+    ve_m = lde(v, y0 - 1);
+    ve_c = lde(v, y0);
+#pragma unroll
+    for (int q = 0; q < PD; ++q) {
+      ueq[q] = lde(u, y0 + 1 + q);
+      veq[q] = lde(v, y0 + 1 + q);
+    }
+  }
   for (int j = y0; j < y1; ++j) {
     const double2 up = uq[0], vp = vq[0];
 #pragma unroll
@@ -164,9 +186,29 @@ __global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const dou
     }
     uq[PD - 1] = ldc(u, j + 1 + PD);
     vq[PD - 1] = ldc(v, j + 1 + PD);
-    const double uWa = dpp_from_left(uc.y), uEb = dpp_from_right(uc.x);
-    const double vEb = dpp_from_right(vc.x), vmEb = dpp_from_right(vm.x);
-    const double vWa = dpp_from_left(vc.y), upWa = dpp_from_left(up.y);
+    double uep = 0.0, vep = 0.0;
+    if (EDGEL) {
+      uep = ueq[0];
+      vep = veq[0];
+#pragma unroll
+      for (int q = 0; q + 1 < PD; ++q) {
+        ueq[q] = ueq[q + 1];
+        veq[q] = veq[q + 1];
+      }
+      ueq[PD - 1] = lde(u, j + 1 + PD);
+      veq[PD - 1] = lde(v, j + 1 + PD);
+    }
+    double uWa = dpp_from_left(uc.y), uEb = dpp_from_right(uc.x);
+    double vEb = dpp_from_right(vc.x), vmEb = dpp_from_right(vm.x);
+    double vWa = dpp_from_left(vc.y), upWa = dpp_from_left(up.y);
+    if (EDGEL) {  // the tile's outer neighbours (same values, so the same bits)
+      uWa = lane == 0 ? ue_c : uWa;
+      vWa = lane == 0 ? ve_c : vWa;
+      upWa = lane == 0 ? uep : upWa;
+      uEb = lane == 63 ? ue_c : uEb;
+      vEb = lane == 63 ? ve_c : vEb;
+      vmEb = lane == 63 ? ve_m : vmEb;
+    }
     double* usr = us + (size_t)(j - g.row_lo) * P;
     double* vsr = vs + (size_t)(j - g.row_lo) * P;
     double usv[2], vsv[2];
@@ -232,6 +274,11 @@ __global__ __launch_bounds__(256) void tentative_kernel(Geo g, Coef c, const dou
       if (vb) vsr[gi + 1] = vsv[1];
     }
     um = uc; uc = up; vm = vc; vc = vp;
+    if (EDGEL) {
+      ue_c = uep;
+      ve_m = ve_c;
+      ve_c = vep;
+    }
   }
 }
 

@@ -289,9 +289,10 @@ def test_log_lines_match_reference_format():
 
 
 @pytest.mark.parametrize("strips", [1, 2])
-@pytest.mark.parametrize("nx", [111, 112, 113, 224, 300])
+@pytest.mark.parametrize("nx", [111, 112, 113, 126, 127, 128, 129, 224, 254, 255, 256, 300])
 def test_cavity_column_tile_widths(nx, strips):
-    """The cavity's column-tiled passes (tentative_kernel: 112-column tiles;
+    """The cavity's column-tiled passes (tentative_kernel: 128-column tiles
+    whose outer neighbours come from extra edge loads;
     cavity_source_kernel + max|f|: 128-column pairs) at widths on and next to
     a tile edge, bit-exact vs the oracle. ny = 190 keeps the grid off the
     one-workgroup path; a capped solve in each ordering checks the tolerance

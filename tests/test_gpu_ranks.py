@@ -175,3 +175,28 @@ def test_proof_mode_on_ranks(world, nx, ny, steps, cap):
         first = 0 if j0 == 1 else j0
         last = min(j1 + 1 if j1 == cp.ny else j1, ref.shape[0] - 1)
         assert np.array_equal(r["p"].view(np.int64), ref[first:last + 1].view(np.int64))
+
+
+@pytest.mark.parametrize("case,world,nx,ny,steps,cap", [("channel", 2, 300, 160, 3, 0), ("channel", 3, 256, 200, 2, 900),
+                                                        ("backwards_step", 2, 400, 160, 2, 0),
+                                                        ("backwards_step", 4, 512, 256, 2, 700)])
+def test_open_proof_mode_on_ranks(case, world, nx, ny, steps, cap):
+    """The open cases' proof-mode launches (open.hip: 4 sweeps for the
+    channel, 3 for the step on ranks) on overlapped ranks with the lagged,
+    all-reduced test, against one domain with exact residuals: iteration
+    counts equal; fields to 1e-9 (the source's mean removal is summed per rank
+    and all-reduced, a re-association)."""
+    kw = {"max_iters": cap} if cap else {}
+    cp = C.make_params(case, nx=nx, ny=ny, **kw)
+    s, its = single(cp, steps, small_solve="off", proof_test="off", tuning={"tile_rounds": 0})
+    ref = {n: s.field(n) for n in ("u", "v", "p")}
+    res = run_ranks(cp, world, steps, proof_test="on")
+    for r in res:
+        assert r["overlapped"] > 0
+        assert [i for i, _ in r["its"]] == [i for i, _ in its]
+        j0, j1 = r["rows"]
+        first = 0 if j0 == 1 else j0
+        for n in ("u", "v", "p"):
+            last = min(j1 + 1 if j1 == cp.ny else j1, ref[n].shape[0] - 1)
+            a, b = r[n], ref[n][first:last + 1]
+            np.testing.assert_allclose(a, b, rtol=0, atol=1e-9 * max(np.abs(b).max(), 1.0))
