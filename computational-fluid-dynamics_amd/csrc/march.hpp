@@ -57,7 +57,13 @@ struct WaveCtx {
   __device__ double2 ld_fast(const double* base, int R) const {
     const int Rc = min(max(R, rmin), rmax);
     const double2* src = reinterpret_cast<const double2*>(base + (size_t)(Rc - g.row_lo) * (size_t)g.pitch + gi);
+#if CFD_NT_LOAD  // (A/B build option: streamed loads)
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v v = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(src));
+    return make_double2(v.x, v.y);
+#else
     return *src;
+#endif
   }
 };
 
