@@ -370,4 +370,28 @@ __device__ __forceinline__ double proof_ratio_gen(const Coef& c, double tol, dou
 }
 
 
+// The SOR launches' p_out rows. CFD_WT_STORE 1: written through (sc1 buffer
+// stores): no dirty lines stay in the XCD's L2 at the kernel's end, which the
+// next dependent launch would otherwise wait for (MI355X_MICROARCH.md,
+// "boundary": + bytes / 6 TB/s). 0: streamed (nt) stores, kept in L2.
+#ifndef CFD_WT_STORE
+#define CFD_WT_STORE 0
+#endif
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(double* base, const Geo& g) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)((size_t)g.nrows * (size_t)g.pitch * sizeof(double)),
+                                           0x00020000);
+}
+__device__ __forceinline__ void store_row_pair(double* base, __amdgpu_buffer_rsrc_t r, size_t off, double2 v) {
+#if CFD_WT_STORE
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r, (int)(off * sizeof(double)), 0, 16);
+  (void)base;
+#else
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  d2v mv = {v.x, v.y};
+  __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(base + off));
+  (void)r;
+#endif
+}
+
 }  // namespace cfd

@@ -28,6 +28,7 @@ struct WaveCtx {
   const Coef& c;  // kernel-argument memory
   const double* pin;
   double* pout;
+  __amdgpu_buffer_rsrc_t prs;  // pout as a buffer resource (store_row_pair)
   const double* f;
   int gi, gic, y0, y1, rmin, rmax;
   int py0 = 0, py1 = 0;  // proof mode: rows [py0, py1) whose black cells prove (band rows, 1 <= j < ny)
@@ -154,6 +155,7 @@ __device__ __forceinline__ double wave_march_ring(const Geo& g, const Coef& c, c
   constexpr int H = 4;
   WaveCtx<CASE> x{g, c};
   x.pin = pin; x.pout = pout; x.f = f;
+  x.prs = out_rsrc(pout, g);
   x.gi = gi;
   x.y0 = y0;
   x.y1 = y1;
@@ -402,16 +404,8 @@ __device__ __forceinline__ void pair_stages(const WaveCtx<CASE>& x, double2 (&W)
     if (jout) {
       const double2 m = Q[CFD_SLOT(4 + OFF)], bh = Q[CFD_SLOT(5 + OFF)], ah = Q[CFD_SLOT(3 + OFF)];
       const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
-      if (store && x.out_lane) {
-        double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
-#ifndef CFD_NO_NT_STORE
-        typedef double d2v __attribute__((ext_vector_type(2)));
-        d2v mv = {m.x, m.y};
-        __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));  // streamed: keep L2 for the re-read halo rows
-#else
-        *dst = m;
-#endif
-      }
+      if (store && x.out_lane)
+        store_row_pair(x.pout, x.prs, (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi, m);
       if (FAST) {
         if (!RC || (j >= x.g.j0 && j <= x.g.j1 && j <= x.res_hi)) {  // row-uniform
           if (CASE == CAVITY && j == ny) {  // top row: eps_n = 0 (cavity-01.cpp:666)
@@ -652,28 +646,15 @@ __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const dou
 #define CFD_N(b, a) ((DIR > 0) ? (a) : (b))
   if (PROOF) {  // no residual: the store of the last sweep
     (void)rm;
-    if (store && j >= x.y0 && j < x.y1 && x.out_lane) {
-      const double2 m = W[CFD_SLOT(X)];
-      double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
-      typedef double d2v __attribute__((ext_vector_type(2)));
-      d2v mv = {m.x, m.y};
-      __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
-    }
+    if (store && j >= x.y0 && j < x.y1 && x.out_lane)
+      store_row_pair(x.pout, x.prs, (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi, W[CFD_SLOT(X)]);
     return;
   }
   if (j >= x.y0 && j < x.y1) {  // row-uniform
     const double2 m = W[CFD_SLOT(X)], bh = W[CFD_SLOT(X + 1)], ah = W[CFD_SLOT(X - 1)];
     const double Lb = dpp_from_left(m.y), Ra = dpp_from_right(m.x);
-    if (store && x.out_lane) {
-      double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
-#ifndef CFD_NO_NT_STORE
-      typedef double d2v __attribute__((ext_vector_type(2)));
-      d2v mv = {m.x, m.y};
-      __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));  // streamed: keep L2 for re-read halo rows
-#else
-      *dst = m;
-#endif
-    }
+    if (store && x.out_lane)
+      store_row_pair(x.pout, x.prs, (size_t)(j - x.g.row_lo) * (size_t)x.g.pitch + x.gi, m);
     if (j >= x.g.j0 && j <= x.g.j1) {
       if (EDGE) {
         const bool top = j == ny;
@@ -929,6 +910,7 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
   if (y0 >= y1) return;
   WaveCtx<CASE> x{g, c};
   x.pin = pin; x.pout = pout; x.f = f;
+  x.prs = out_rsrc(pout, g);
   x.gi = gi;
   x.y0 = y0;
   x.y1 = y1;

@@ -212,10 +212,7 @@ __device__ __forceinline__ void open_sweeps(const WaveCtx<CASE>& x, const OpenLa
         if (RC)
           v = open_refresh<CASE, EDGE, 3>(x, L, js, v, open_lo<DIR, ROT>(s.w[S], 2 * S + 3),
                                           open_hi<DIR, ROT>(s.w[S], 2 * S + 3));
-        double2* dst = reinterpret_cast<double2*>(x.pout + (size_t)(js - x.g.row_lo) * (size_t)x.g.pitch + x.gi);
-        typedef double d2v __attribute__((ext_vector_type(2)));
-        d2v mv = {v.x, v.y};
-        __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
+        store_row_pair(x.pout, x.prs, (size_t)(js - x.g.row_lo) * (size_t)x.g.pitch + x.gi, v);
       }
     }
     open_sweeps<S + 1, NS, CASE, DIR, ROT, PAR, EDGE, RC>(x, L, s, R);
@@ -345,6 +342,7 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
   if (y0 >= y1) return;
   WaveCtx<CASE> x{g, c};
   x.pin = pin; x.pout = pout; x.f = f;
+  x.prs = out_rsrc(pout, g);
   x.gi = gi;
   x.y0 = y0;
   x.y1 = y1;
