@@ -50,6 +50,7 @@ struct Coef {
   double h2;               // cavity: grid_spacing * grid_spacing
   double denom;            // open cases: 2*(idx2+idy2)
   double rdenom;           // open cases: 1.0 / denom (correctly rounded, host)
+  double rdenom_lo;        // open cases: RN((1 - rdenom*denom) / denom): rdenom + rdenom_lo ~ 1/denom to 2^-106
   double cav_src;          // cavity: (1/dt) * rho           (cavity-01.cpp:624)
   double open_src;         // open:   rho / dt               (channel-01.cpp:610)
   double cav_corr;         // cavity: (dt/h) * rho           (cavity-01.cpp:696,701)
@@ -159,19 +160,21 @@ __device__ __forceinline__ double dpp_from_right(double v) {  // lane l receives
 // Ghost / solid refresh after each sweep: channel-01.cpp:531-541,
 // backwards_step-01.cpp:685-740.
 
-// x / denom, correctly rounded, without the divide sequence: q0 = RN(x*y)
-// with y = RN(1/denom), then two FMA corrections q <- RN(q + RN(x - q*denom)*y)
-// (the residual x - q*denom is exact in an FMA). After the first correction
-// q is a faithful quotient (relative error ~2^-105 before rounding), and y has
-// relative error below 2^-53, so by Markstein's theorem the second correction
-// returns RN(x/denom). denom > 0, so the quotient has x's sign (the copysign
-// keeps -0/denom = -0, which the corrections would turn into +0). Finite,
-// normal operands (pressure sums): no over/underflow. Checked against the
-// hardware divide in tests/test_division.py (random and adversarial denominators).
+// x / denom, correctly rounded, without the divide sequence. y = RN(1/denom)
+// and ylo = RN((1 - y*denom)/denom) (host; 1 - y*denom is exact), so y + ylo
+// is 1/denom to ~2^-106 relative: q0 = RN(x*y + RN(x*ylo)) is within 2^-105
+// relative of x/denom before its rounding, hence a faithful quotient. One FMA
+// correction q = RN(q0 + RN(x - q0*denom)*y) (the residual is exact in an FMA
+// for a faithful q0) then returns RN(x/denom) by Markstein's theorem (y has
+// relative error below 2^-53). Four operations; the former form (q0 = RN(x*y)
+// and two corrections) took five. denom > 0, so the quotient has x's sign
+// (the copysign keeps -0/denom = -0, which the correction turns into +0).
+// Finite, normal operands (pressure sums): no over/underflow. Checked against
+// the IEEE divide in tests/test_division.py (random and adversarial
+// denominators, quotients next to rounding midpoints).
 __device__ __forceinline__ double div_denom(const Coef& c, double x) {
   const double d = c.denom, y = c.rdenom;
-  double q = x * y;
-  q = fma(fma(-q, d, x), y, q);
+  double q = fma(x, y, x * c.rdenom_lo);
   q = fma(fma(-q, d, x), y, q);
   return copysign(q, x);
 }

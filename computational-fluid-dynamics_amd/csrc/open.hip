@@ -291,6 +291,16 @@ __device__ __forceinline__ void open_march(const WaveCtx<CASE>& x, int y0, int y
 #ifndef CFD_OPEN_MIN_WAVES
 #define CFD_OPEN_MIN_WAVES 2
 #endif
+// diagnostic build only (CFD_OPEN_STAMPS=1, never the product library): each
+// wave's march duration (shader clock) with its tile, band and path, read
+// back by cfd_open_stamps (the last launch's)
+#ifndef CFD_OPEN_STAMPS
+#define CFD_OPEN_STAMPS 0
+#endif
+#if CFD_OPEN_STAMPS
+constexpr int OPEN_STAMP_MAX = 8192;
+__device__ long long open_stamp_buf[OPEN_STAMP_MAX * 8];
+#endif
 
 // Tiling as poisson_multi_kernel (PairPlan: boundary-column tiles in bands of
 // pl.the rows, then the interior column tiles; 8-column halos, 112 output
@@ -371,6 +381,10 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
   // interior band whose march stays in rows 1 .. ny (no ghost row, stored
   // rows only): no row checks, nothing refreshed
   const bool safe = cols_in && y0 - CONE > x.rmin && y1 + CONE < min(x.rmax, g.ny + 1);
+#if CFD_OPEN_STAMPS
+  long long t0_;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0_)::"memory");
+#endif
   double dm[NS], pm = 0.0;
   if (!cols_in) open_march<NS, CASE, 1, true, true>(x, y0, y1, dm, pm);
   else if (safe && up) open_march<NS, CASE, -1, false, false>(x, y0, y1, dm, pm);
@@ -384,6 +398,19 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
   double r[NS];
 #pragma unroll
   for (int q = 0; q < NS; ++q) r[q] = proof_ratio_gen(c, tol, wave_max(dm[q]), pinv, F, growth);
+#if CFD_OPEN_STAMPS
+  {
+    long long t1_;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_)::"memory");
+    if (tile < OPEN_STAMP_MAX && lane < 8) {
+      const long long v[8] = {tile, ctile, band, y0, y1, cols_in ? 1 : 0, safe ? 1 : 0, t1_ - t0_};
+      long long o = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o = lane == q ? v[q] : o;
+      open_stamp_buf[(size_t)tile * 8 + lane] = o;
+    }
+  }
+#endif
   if (lane == 0) {
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
@@ -393,6 +420,16 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
     }
   }
 }
+
+#if CFD_OPEN_STAMPS
+// diagnostic build only: per wave {tile, column tile, band, y0, y1, interior
+// columns, safe, cycles} of the last open proof launch
+extern "C" int cfd_open_stamps(long long* out, int n) {
+  if (n > OPEN_STAMP_MAX * 8) n = OPEN_STAMP_MAX * 8;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(open_stamp_buf), (size_t)n * 8) == hipSuccess ? n : -1;
+}
+#endif
 
 void open_proof_launch(int case_id, int ns, const Geo& g, const Coef& c, const double* pin, double* pout,
                        const double* f, const PoissonCtl& ctl, int k, int ka, int kb, const PairPlan& pl, int flags,

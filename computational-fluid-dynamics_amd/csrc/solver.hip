@@ -73,6 +73,7 @@ static Coef make_coef(const cfd_params& p) {
   c.h2 = p.dx * p.dx;
   c.denom = 2.0 * (c.idx2 + c.idy2);
   c.rdenom = 1.0 / c.denom;
+  c.rdenom_lo = std::fma(-c.rdenom, c.denom, 1.0) / c.denom;  // (device.hpp div_denom)
   c.cav_src = (1.0 / p.dt) * p.rho;
   c.open_src = p.rho / p.dt;
   c.cav_corr = (p.dt / p.dx) * p.rho;

@@ -21,10 +21,19 @@ __device__ __forceinline__ bool tile_refreshes(const Coef& c, int nx, int ny, in
 #ifndef CFD_TILE_FENCE
 #define CFD_TILE_FENCE 1
 #endif
+// rows per scheduling group (CFD_TILE_FENCE_ROWS): the rows of a group are
+// scheduled together (their LDS loads issued before their arithmetic: two
+// independent chains in flight per wave)
+#ifndef CFD_TILE_FENCE_ROWS
+#define CFD_TILE_FENCE_ROWS 1
+#endif
 #if CFD_TILE_FENCE
-#define TILE_ROW_FENCE() __builtin_amdgcn_sched_barrier(0)
+#define TILE_ROW_FENCE(q)                                                    \
+  do {                                                                       \
+    if (((q) + 1) % CFD_TILE_FENCE_ROWS == 0) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
 #else
-#define TILE_ROW_FENCE() ((void)0)
+#define TILE_ROW_FENCE(q) ((void)0)
 #endif
 // 1: each wave owns a contiguous band of region rows and marches it, rows
 // j-1 and j kept in registers (one LDS row load per row and phase instead of
@@ -33,6 +42,29 @@ __device__ __forceinline__ bool tile_refreshes(const Coef& c, int nx, int ny, in
 // sequential chain of LDS loads is latency-bound)
 #ifndef CFD_TILE_BAND
 #define CFD_TILE_BAND 0
+#endif
+// diagnostic build only (CFD_TILE_STAMPS=1, never the product library): each
+// wave sums the shader-clock cycles of its phases (load, red, red barrier,
+// black, black barrier, refresh, residual, store) over the launch's sweeps
+// into a buffer of its own, read back by cfd_tile_stamps (shares, not times:
+// the stamps' waits forbid overlaps the real kernel has)
+#ifndef CFD_TILE_STAMPS
+#define CFD_TILE_STAMPS 0
+#endif
+#if CFD_TILE_STAMPS
+constexpr int STAMP_SEGS = 8;
+__device__ unsigned long long tile_stamp_buf[1024 * TILE_WAVES * STAMP_SEGS];
+#define TILE_STAMP(seg)                                                                     \
+  do {                                                                                      \
+    unsigned long long t_;                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
+    __builtin_amdgcn_sched_barrier(0);                                                      \
+    st_acc[seg] += t_ - st_last;                                                            \
+    st_last = t_;                                                                           \
+  } while (0)
+#else
+#define TILE_STAMP(seg) ((void)0)
 #endif
 
 template <int CASE, bool PROOF>
@@ -48,6 +80,10 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
   double* Pd = reinterpret_cast<double*>(P);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if CFD_TILE_STAMPS
+  unsigned long long st_acc[STAMP_SEGS] = {}, st_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
 
   const int nblk = (int)gridDim.x;
   const int L8 = (nblk / 8) * 8;
@@ -71,6 +107,27 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
   const int r0 = BAND ? w * RB : w;
   const int rend = BAND ? min(r0 + RB, RH) : RH;
   auto row = [&](int q) { return BAND ? r0 + q : w + TILE_WAVES * q; };
+  // the same rows from a base made opaque at the start of each phase: the
+  // row-uniform conditions below are then recomputed per phase in SALU
+  // instead of being hoisted out of the sweep loop as live SGPR masks (8 rows
+  // x 2 colours of them spilled to VGPR lanes: v_readlane / v_writelane,
+  // i.e. VALU work in every row)
+  auto phase_rows = [&]() {
+    int b = BAND ? r0 : w;
+    asm volatile("" : "+s"(b));
+    return b;
+  };
+  auto prow_q = [&](int b, int q) { return BAND ? b + q : b + TILE_WAVES * q; };
+  // interleaved rows: row r's C / S / N, the row clamped into the region
+  // (rows 0 and RH-1 are read, never updated). (Issuing each row's loads one
+  // row ahead does not survive compilation: the optimiser sinks the current
+  // row's loads into its branch, behind the next row's, and waits for both.)
+  auto ld3 = [&](int r, double2& C, double2& S, double2& N) {
+    const int rc = min(max(r, 1), RH - 2);
+    C = P[rc * 64 + lane];
+    S = P[(rc - 1) * 64 + lane];
+    N = P[(rc + 1) * 64 + lane];
+  };
 
   // p_in into LDS, f of this wave's rows into registers (rows / columns
   // clamped to stored memory: clamped cells lie outside the grid and are
@@ -115,6 +172,7 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
   }
   __syncthreads();  // (also: the LDS tile written)
   if (!go) return;
+  TILE_STAMP(0);
 
   const bool refr = CASE != CAVITY && tile_refreshes(c, nx, ny, gy0, RH, x0 - TILE_H);
   // lane constants of the two columns (slot a: gx, slot b: gx + 1): updated
@@ -167,9 +225,10 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
         if (r0 >= 1 && r0 - 1 < RH) Sv = P[(r0 - 1) * 64 + lane];
         if (r0 < RH) Cv = P[r0 * 64 + lane];
       }
+      const int rb = phase_rows();
 #pragma unroll
       for (int q = 0; q < TILE_RPW; ++q) {
-        const int r = row(q);
+        const int r = prow_q(rb, q);
         const int j = gy0 + r;
         if (!(r < rend)) break;
         double2 C = Cv, S = Sv, N = z2;
@@ -177,10 +236,8 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
           if (r + 1 < RH) N = P[(r + 1) * 64 + lane];
           Sv = Cv;
           Cv = N;
-        } else if (r >= 1 && r <= RH - 2) {
-          C = P[r * 64 + lane];
-          S = P[(r - 1) * 64 + lane];
-          N = P[(r + 1) * 64 + lane];
+        } else {
+          ld3(r, C, S, N);
         }
         // region rows with both neighbours in LDS, grid rows that are updated
         if (r >= 1 && r <= RH - 2 && j >= 1 && j <= ny && j > rmin && j < rmax) {
@@ -204,13 +261,15 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
             if (PROOF && prow && prv_b && (pstep || !nb_b)) dmx = fmax(dmx, fabs(nv - C.y));
           }
         }
-        TILE_ROW_FENCE();
+        TILE_ROW_FENCE(q);
       }
+      TILE_STAMP(1 + 2 * col);
       if (PROOF && col == 1) {
         dmx = wave_max(dmx);
         if (lane == 0) wred[w] = dmx;
       }
       __syncthreads();
+      TILE_STAMP(2 + 2 * col);
     }
     if (PROOF && w == 0) {  // this sweep's ratio (wred: written before the barrier above, rewritten after the next)
       double v = lane < TILE_WAVES ? wred[lane] : 0.0, pv = lane < TILE_WAVES ? pinw[lane] : 0.0;
@@ -230,9 +289,10 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
     // first (from interior cells, none of which changes here), then the
     // step's solid cells next to fluid (from fluid cells only)
     if (CASE != CAVITY && refr) {
+      const int rg = phase_rows();
 #pragma unroll
       for (int q = 0; q < TILE_RPW; ++q) {
-        const int r = row(q);
+        const int r = prow_q(rg, q);
         const int j = gy0 + r;
         if (r < rend && r >= 1 && r <= RH - 2 && j >= 0 && j <= ny + 1) {
           double* pa = Pd + (r * 64 + lane) * 2;
@@ -249,9 +309,10 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
       }
       __syncthreads();
       if (CASE == BACKSTEP) {
+        const int rs = phase_rows();
 #pragma unroll
         for (int q = 0; q < TILE_RPW; ++q) {
-          const int r = row(q);
+          const int r = prow_q(rs, q);
           const int j = gy0 + r;
           if (r < rend && r >= 1 && r <= RH - 2 && j > c.inlet_jmax && j <= ny) {  // rows of the solid block
             const double2 C = P[r * 64 + lane], S = P[(r - 1) * 64 + lane], N = P[(r + 1) * 64 + lane];
@@ -268,6 +329,7 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
         __syncthreads();
       }
     }
+    TILE_STAMP(5);
     // max-norm residual over the owned fluid cells (cavity-01.cpp:659-677,
     // channel-01.cpp:672-681, backwards_step-01.cpp:916-930) -> ring slot k+s
     if (PROOF) continue;
@@ -278,9 +340,10 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
       if (r0 >= 1 && r0 - 1 < RH) Sv = P[(r0 - 1) * 64 + lane];
       if (r0 < RH) Cv = P[r0 * 64 + lane];
     }
+    const int rr = phase_rows();
 #pragma unroll
     for (int q = 0; q < TILE_RPW; ++q) {
-      const int r = row(q);
+      const int r = prow_q(rr, q);
       const int j = gy0 + r;
       if (!(r < rend)) break;
       double2 C = Cv, S = Sv, N = z2;
@@ -289,10 +352,8 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
         if (r + 1 < RH) N = P[(r + 1) * 64 + lane];
         Sv = Cv;
         Cv = N;
-      } else if (resrow) {
-        C = P[r * 64 + lane];
-        S = P[(r - 1) * 64 + lane];
-        N = P[(r + 1) * 64 + lane];
+      } else {
+        ld3(r, C, S, N);
       }
       if (resrow) {
         const bool open = CASE != BACKSTEP || j <= c.inlet_jmax;
@@ -308,7 +369,7 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
         }
         m = fmax(m, fmax((own_a && (open || !blk_a)) ? ra : 0.0, (own_b && (open || !blk_b)) ? rb : 0.0));
       }
-      TILE_ROW_FENCE();
+      TILE_ROW_FENCE(q);
     }
     m = wave_max(m);
     if (lane == 0) wred[w] = m;
@@ -322,6 +383,7 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
                   (unsigned long long)__double_as_longlong(v));
       }
     }
+    TILE_STAMP(6);
   }
   // owned cells -> p_out (16-B pairs; columns up to the pitch)
   const bool st_lane = 2 * lane >= TILE_H && 2 * lane < TILE_H + TILE_W && gx >= 0 && gx + 1 < g.pitch;
@@ -332,6 +394,16 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
     if (r < rend && j >= y0 && j < y1 && st_lane)
       *reinterpret_cast<double2*>(pout + (size_t)(j - g.row_lo) * (size_t)g.pitch + (size_t)gx) = P[r * 64 + lane];
   }
+#if CFD_TILE_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);  // (the stores issued: their issue time, not their completion)
+  TILE_STAMP(7);
+  if (lane < STAMP_SEGS && bl < 1024) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int q = 0; q < STAMP_SEGS; ++q) v = lane == q ? st_acc[q] : v;
+    tile_stamp_buf[((size_t)bl * TILE_WAVES + w) * STAMP_SEGS + lane] = v;
+  }
+#endif
 }
 
 TilePlan tile_plan(int nx, int lo, int hi, int max_tiles) {
@@ -366,5 +438,16 @@ void tile_launch(int case_id, bool proof, const Geo& g, const Coef& c, const dou
   }
 #undef CFD_TILE_LAUNCH
 }
+
+#if CFD_TILE_STAMPS
+// diagnostic build only: the last tile launch's per-wave phase cycle sums,
+// [block][wave][segment] (1024 x TILE_WAVES x 8 values)
+extern "C" int cfd_tile_stamps(unsigned long long* out, int n) {
+  const int cap = 1024 * TILE_WAVES * STAMP_SEGS;
+  if (n > cap) n = cap;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(tile_stamp_buf), (size_t)n * 8) == hipSuccess ? n : -1;
+}
+#endif
 
 }  // namespace cfd

@@ -1,8 +1,13 @@
-/* Bit-exactness check of the divide used by the open-case SOR kernels
- * (kernels.hpp div_denom): x / d computed as q = RN(x*y), y = RN(1/d), then two
- * FMA corrections q <- RN(q + RN(x - q*d)*y), sign of x. Compared with the
- * IEEE divide (x / d) on random numerators over +-100 binades, for the
- * denominators of the BASELINE configs and random / adversarial ones
+/* Bit-exactness check of the divides used by the open-case SOR kernels
+ * (device.hpp div_denom), y = RN(1/d), sign of x restored at the end:
+ *  - two:   q = RN(x*y), then two FMA corrections q <- RN(q + RN(x - q*d)*y);
+ *  - split: q = RN(x*y + RN(x*ylo)) with ylo = RN((1 - y*d)/d) (a faithful
+ *           quotient), then one correction;
+ *  - one:   q = RN(x*y), one correction - only for denominators with
+ *           |1 - y*d| <= 2^-54 (RN(x*y) is then faithful).
+ * Compared with the IEEE divide (x / d) on random numerators over +-100
+ * binades and on numerators whose quotient lies next to a rounding midpoint,
+ * for the denominators of the BASELINE configs and random / adversarial ones
  * (significands with long runs of ones). Prints mismatches; exit 1 if any.
  * usage: division_check SAMPLES_PER_DENOMINATOR RANDOM_DENOMINATORS */
 #include <math.h>
@@ -29,6 +34,16 @@ static double div_denom(double x, double d, double y) {
   q = fma(fma(-q, d, x), y, q);
   return copysign(q, x);
 }
+static double div_split(double x, double d, double y, double ylo) {
+  double q = fma(x, y, x * ylo);
+  q = fma(fma(-q, d, x), y, q);
+  return copysign(q, x);
+}
+static double div_one(double x, double d, double y) {
+  double q = x * y;
+  q = fma(fma(-q, d, x), y, q);
+  return copysign(q, x);
+}
 static double denom_of(int nx, int ny, double lx, double ly) {
   const double dx = lx / nx, dy = ly / ny;
   const double idx2 = 1.0 / (dx * dx), idy2 = 1.0 / (dy * dy);
@@ -44,7 +59,7 @@ int main(int argc, char** argv) {
                     denom_of(256, 32, 8.0, 1.0), 3.0, 7.0, 10.0, 0.1, 1.0 / 3.0, bits(0x3fffffffffffffffull),
                     bits(0x3ff0000000000001ull)};
   const int nf = (int)(sizeof fixed / sizeof fixed[0]);
-  long bad = 0, n = 0;
+  long bad = 0, n = 0, n_one = 0;
   for (int k = 0; k < nf + nrand; ++k) {
     double d;
     if (k < nf) {
@@ -55,22 +70,38 @@ int main(int argc, char** argv) {
       d = ldexp(bits(b), (int)(xr() % 60) - 30);
     }
     const double y = 1.0 / d;
+    const double r = fma(-y, d, 1.0); /* exact */
+    const double ylo = r / d;
+    const int one_ok = fabs(r) <= 0x1p-54;
+    n_one += one_ok;
     for (long t = 0; t < per; ++t) {
-      const uint64_t b = (xr() & 0x800fffffffffffffull) | ((uint64_t)(1023 + (int)(xr() % 200) - 100) << 52);
-      const double x = bits(b);
-      const double a = x / d, m = div_denom(x, d, y);
-      if (memcmp(&a, &m, 8) != 0) {
-        if (bad < 5) printf("mismatch d=%a x=%a div=%a fma=%a\n", d, x, a, m);
-        ++bad;
+      double x;
+      if (t % 4 == 3) { /* quotient next to a midpoint: x = RN(m*d), m = odd 54-bit significand */
+        const uint64_t mm = (xr() & 0x1fffffffffffffull) | 0x20000000000000ull | 1ull;
+        const int k = (int)(xr() % 120) - 60 - 53;
+        x = fma((double)(mm >> 1), ldexp(d, k + 1), ldexp(d, k)); /* RN(mm * 2^k * d), one rounding */
+        if (xr() & 1) x = -x;
+      } else {
+        const uint64_t b = (xr() & 0x800fffffffffffffull) | ((uint64_t)(1023 + (int)(xr() % 200) - 100) << 52);
+        x = bits(b);
       }
+      const double a = x / d;
+      const double m[3] = {div_denom(x, d, y), div_split(x, d, y, ylo), one_ok ? div_one(x, d, y) : a};
+      for (int v = 0; v < 3; ++v)
+        if (memcmp(&a, &m[v], 8) != 0) {
+          if (bad < 5) printf("mismatch (variant %d) d=%a x=%a div=%a fma=%a\n", v, d, x, a, m[v]);
+          ++bad;
+        }
       ++n;
     }
     const double zs[2] = {0.0, -0.0};
     for (int z = 0; z < 2; ++z) {
-      const double a = zs[z] / d, m = div_denom(zs[z], d, y);
-      if (memcmp(&a, &m, 8) != 0) ++bad;
+      const double a = zs[z] / d, m0 = div_denom(zs[z], d, y), m1 = div_split(zs[z], d, y, ylo),
+                   m2 = div_one(zs[z], d, y);
+      if (memcmp(&a, &m0, 8) != 0 || memcmp(&a, &m1, 8) != 0 || memcmp(&a, &m2, 8) != 0) ++bad;
     }
   }
+  printf("one-correction denominators: %ld of %d\n", n_one, nf + nrand);
   printf("%ld mismatches of %ld\n", bad, n);
   return bad != 0;
 }

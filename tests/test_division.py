@@ -1,5 +1,7 @@
-"""The open-case SOR divide (kernels.hpp div_denom: reciprocal + two FMA
-corrections) is bit-identical to the IEEE divide the reference performs
+"""The open-case SOR divide (device.hpp div_denom: split reciprocal + one FMA
+correction; the former two-correction form and the one-correction form for
+denominators with |1 - y*d| <= 2^-54 alongside) is bit-identical to the IEEE
+divide the reference performs
 (channel-01.cpp:663, backwards_step-01.cpp:908): random numerators over
 +-100 binades for the config denominators and random / adversarial ones.
 CPU only (gcc, hardware FMA); the GPU path is covered bit-for-bit by the
