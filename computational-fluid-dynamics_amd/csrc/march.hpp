@@ -832,12 +832,27 @@ struct PairPlan {
   int the, nbe0, nbe1; // boundary column tiles
   int lo0, hi0, lo1, hi1;
   int cxa, cxb;        // step: column tiles across the step's column (+1; 0: none), banded like the boundary ones
+  // step, proof launches (open.hip) only: column tiles 1..nl lie left of the
+  // step's column. Below the block: nlf bands of th rows over [lo0, lz) march
+  // the interior-column path (away from the block edge), nle bands of `the`
+  // rows over [lz, le) the masked one, le = inlet_jmax + 2 (the block's lower
+  // edge row included); then nlt bands of `the` rows over [lt, hi0) when the
+  // range holds ghost row ny + 1 (refreshed from the block's top row). The
+  // block's interior rows between never change (both buffers hold them).
+  // nl = 0: no such class.
+  int nl, nlf, nle, nlt, lz, le, lt;
 };
 
 // column tiles banded as boundary tiles (masked march): the first and last,
 // and the step's mixed ones
 __host__ __device__ inline int plan_edge_tiles(const PairPlan& pl) {
   return (pl.ctiles >= 2 ? 2 : 1) + (pl.cxa > 0) + (pl.cxb > 0);
+}
+
+// waves of a plan (every class)
+__host__ __device__ inline int plan_waves(const PairPlan& pl) {
+  const int ne = plan_edge_tiles(pl);
+  return ne * (pl.nbe0 + pl.nbe1) + pl.nl * (pl.nlf + pl.nle + pl.nlt) + (pl.ctiles - ne - pl.nl) * (pl.nb0 + pl.nb1);
 }
 
 // PROOF (cavity): the convergence test of each sweep is the proof above

@@ -326,29 +326,44 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
   const int tile = blk * 4 + wv;
   const int ne = (pl.ctiles >= 2) ? 2 : 1;
   const int ned = plan_edge_tiles(pl);
-  const int nbe = pl.nbe0 + pl.nbe1, nbi = pl.nb0 + pl.nb1;
-  int band, ctile, th, nb0;
+  const int nbe = pl.nbe0 + pl.nbe1, nbi = pl.nb0 + pl.nb1, nlb = pl.nlf + pl.nle + pl.nlt;
+  int band, ctile, y0, y1;
+  // band `band` of a class with bands of th rows: nb0 of them over [lo0, hi0), then [lo1, hi1)
+  auto rows_of = [&](int th, int nb0) {
+    const bool r0 = band < nb0;
+    y0 = r0 ? pl.lo0 + band * th : pl.lo1 + (band - nb0) * th;
+    y1 = min(y0 + th, r0 ? pl.hi0 : pl.hi1);
+  };
   if (tile < ned * nbe) {
     const int e = tile / nbe;
     ctile = (e == 0) ? 0 : (e == 1 && ne == 2) ? pl.ctiles - 1 : (e == ne && pl.cxa > 0) ? pl.cxa - 1 : pl.cxb - 1;
     band = tile % nbe;
-    th = pl.the;
-    nb0 = pl.nbe0;
-  } else {
+    rows_of(pl.the, pl.nbe0);
+  } else if (tile < ned * nbe + pl.nl * nlb) {  // step: left of the step's column
     const int t = tile - ned * nbe;
-    const int nci = pl.ctiles - ned;
+    ctile = 1 + t % pl.nl;
+    band = t / pl.nl;
+    if (band < pl.nlf) {
+      y0 = pl.lo0 + band * pl.th;
+      y1 = min(y0 + pl.th, pl.lz);
+    } else if (band < pl.nlf + pl.nle) {
+      y0 = pl.lz + (band - pl.nlf) * pl.the;
+      y1 = min(y0 + pl.the, pl.le);
+    } else {
+      y0 = pl.lt + (band - pl.nlf - pl.nle) * pl.the;
+      y1 = min(y0 + pl.the, pl.hi0);
+    }
+  } else {
+    const int t = tile - ned * nbe - pl.nl * nlb;
+    const int nci = pl.ctiles - ned - pl.nl;
     if (t >= nci * nbi) return;
-    ctile = 1 + t % nci;
+    ctile = 1 + pl.nl + t % nci;
     band = t / nci;
     if (pl.cxa > 0 && ctile >= pl.cxa - 1) ++ctile;
     if (pl.cxb > 0 && ctile >= pl.cxb - 1) ++ctile;
-    th = pl.th;
-    nb0 = pl.nb0;
+    rows_of(pl.th, pl.nb0);
   }
   const int gi = ctile * PAIR_TWC - H + 2 * lane;
-  const bool r0 = band < nb0;
-  const int y0 = r0 ? pl.lo0 + band * th : pl.lo1 + (band - nb0) * th;
-  const int y1 = min(y0 + th, r0 ? pl.hi0 : pl.hi1);
   if (y0 >= y1) return;
   WaveCtx<CASE> x{g, c};
   x.pin = pin; x.pout = pout; x.f = f;
@@ -369,12 +384,18 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
   x.py0 = max(y0, 2);
   x.py1 = min(y1, g.ny);
   const int c0 = ctile * PAIR_TWC - H;
-  // interior-column wave: every column a fluid cell with fluid neighbours, off the step's block
-  const bool cols_in = c0 >= 1 && c0 + 127 <= g.nx && (CASE != BACKSTEP || c0 > c.step_i + 1);
   constexpr int CONE = 2 * NS + 2;  // rows the march reads beyond its band (pipeline + parity row)
-  if (CASE == BACKSTEP && c0 + 127 <= c.step_i - 1 && y0 - CONE >= c.inlet_jmax + 2 && y1 + CONE <= g.ny) {
-    // a band inside the block, away from fluid and ghost rows: never updated
-    // or refreshed (both buffers hold its values)
+  // interior-column wave: every column a fluid cell with fluid neighbours, off
+  // the step's block: right of the block, or left of the step's column with
+  // every row the march reads below the block's lower edge row (inlet_jmax +
+  // 1, refreshed each sweep: the margin mirrors `safe`'s for ghost row ny + 1)
+  const bool cols_in = c0 >= 1 && c0 + 127 <= g.nx &&
+                       (CASE != BACKSTEP || c0 > c.step_i + 1 ||
+                        (c0 + 127 <= c.step_i - 1 && y1 + CONE < c.inlet_jmax + 1));
+  if (CASE == BACKSTEP && c0 >= 1 && c0 + 127 <= c.step_i - 1 && y0 - CONE >= c.inlet_jmax + 2 &&
+      y1 + CONE <= g.ny) {
+    // a band inside the block, away from fluid and ghost rows / columns:
+    // never updated or refreshed (both buffers hold its values)
     return;
   }
   const bool up = (flags & 1) && (band & 1);
@@ -434,8 +455,7 @@ extern "C" int cfd_open_stamps(long long* out, int n) {
 void open_proof_launch(int case_id, int ns, const Geo& g, const Coef& c, const double* pin, double* pout,
                        const double* f, const PoissonCtl& ctl, int k, int ka, int kb, const PairPlan& pl, int flags,
                        hipStream_t st) {
-  const int ne = plan_edge_tiles(pl);
-  const int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
+  const int ntiles = plan_waves(pl);
   if (ntiles == 0) return;
   const dim3 grid((ntiles + 3) / 4);
 #define CFD_OPEN_LAUNCH(CASE, NS) \

@@ -651,6 +651,9 @@ class Solver {
   // Rows one interior wave marches beyond its band (both sides together, plus
   // the parity alignment row) for an n-sweep launch: the cavity's pipeline has
   // depth 2n+1, the open cases' pair pipeline 7.
+  // an n-sweep launch that runs open.hip's proof march (its plans may carry the step's left class)
+  bool open_proof_n(int n) const { return P.case_id != CFD_CAVITY && n >= 3 && proof_launch; }
+
   int march_extra(int n) const { return (P.case_id == CFD_CAVITY || n == 4) ? 2 * (2 * n + 1) + 1 : 15; }
 
   // Tiling of an n-sweep launch over rows [lo0, hi0) + [lo1, hi1) with at most
@@ -658,8 +661,11 @@ class Solver {
   // rows, marched in groups of 10 over th + march_extra rows, so th + extra is
   // a multiple of 10. The two boundary column tiles march slower (masks):
   // shorter bands, pair_edge_pct % of the interior march.
+  // left_class (the step's proof launches, open.hip): the column tiles left of
+  // the step's column become their own class (PairPlan::nl), banded over the
+  // rows below the block only, with short bands next to its lower edge.
   PairPlan multi_plan(int lo0, int hi0, int lo1, int hi1, int waves, int n, int max_th = 1 << 30,
-                      int edge_pct = -1, int twc = PAIR_TWC, int ex = -1) const {
+                      int edge_pct = -1, int twc = PAIR_TWC, int ex = -1, bool left_class = false) const {
     if (edge_pct < 0) edge_pct = pair_edge_pct;
     PairPlan pl{};
     pl.ctiles = (P.nx + 2 + twc - 1) / twc;
@@ -678,10 +684,26 @@ class Solver {
       }
     }
     const int rows = (hi0 - lo0) + (hi1 - lo1);
-    const int ne = plan_edge_tiles(pl);
     const int rmax = std::max(hi0 - lo0, hi1 - lo1);
     if (ex < 0) ex = march_extra(n);
     auto nbands = [](int lo, int hi, int t) { return hi > lo ? (hi - lo + t - 1) / t : 0; };
+    // the left class: column tiles 1 .. cxa-2 (wholly left of the step's
+    // column); rows [lo0, lz) interior-column bands (every row the march
+    // reads below the block's lower edge row: open.hip cols_in), [lz, le) short
+    const bool lc = left_class && P.case_id == CFD_BACKSTEP && pl.cxa > 2 && hi1 <= lo1;
+    if (lc) {
+      pl.nl = pl.cxa - 2;
+      pl.lz = std::max(lo0, std::min(hi0, C.inlet_jmax - (2 * n + 2)));
+      pl.le = std::max(pl.lz, std::min(hi0, C.inlet_jmax + 2));
+      pl.lt = hi0;  // (ghost row ny + 1 in the range: set with `the` below)
+    }
+    auto left_bands = [&] {
+      if (!lc) return;
+      pl.nlf = nbands(lo0, pl.lz, pl.th);
+      pl.nle = nbands(pl.lz, pl.le, pl.the);
+      if (hi0 == P.ny + 2) pl.lt = std::max(pl.le, hi0 - pl.the);
+      pl.nlt = nbands(pl.lt, hi0, pl.the);
+    };
     int nb = std::max(1, std::min(waves / std::max(1, pl.ctiles), (rows + march_min_th - 1) / march_min_th));
     nb = std::max(nb, (rows + max_th - 1) / max_th);
     for (;; --nb) {  // most interior bands whose tiles (boundary tiles included) fit one round
@@ -693,6 +715,7 @@ class Solver {
         pl.nb1 = nbands(lo1, hi1, pl.th);
         pl.nbe0 = nbands(lo0, hi0, pl.the);
         pl.nbe1 = nbands(lo1, hi1, pl.the);
+        left_bands();
         break;
       }
       pl.the = std::max(8, std::min(rmax, (pl.th + ex) * edge_pct / 100 - ex));
@@ -700,8 +723,8 @@ class Solver {
       pl.nb1 = nbands(lo1, hi1, pl.th);
       pl.nbe0 = nbands(lo0, hi0, pl.the);
       pl.nbe1 = nbands(lo1, hi1, pl.the);
-      const int tiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
-      if (tiles <= waves || nb == 1) break;
+      left_bands();
+      if (plan_waves(pl) <= waves || nb == 1) break;
     }
     return pl;
   }
@@ -714,8 +737,7 @@ class Solver {
     // bit 2: no test at all (the solve has already stopped); bit 7: the tested
     // window holds proof ratios (it was computed by a proof-mode launch)
     const int fl = march_flags | (replay ? 4 : 0) | (window_proof ? 128 : 0);
-    const int ne = plan_edge_tiles(pl);
-    const int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
+    const int ntiles = plan_waves(pl);
     if (ntiles == 0) return;
     const dim3 grid((ntiles + 3) / 4);
     if constexpr (CASE == CAVITY) {
@@ -757,7 +779,8 @@ class Solver {
       const int rows = g.wj1 - g.wj0 + 1;
       int ctiles, th, nbands;
       if (n >= 2) {
-        const PairPlan pl = multi_plan(g.wj0, g.wj1 + 1, 0, 0, resident_pair_waves / (int)S.size(), n);
+        const PairPlan pl = multi_plan(g.wj0, g.wj1 + 1, 0, 0, resident_pair_waves / (int)S.size(), n, 1 << 30, -1,
+                                       PAIR_TWC, -1, open_proof_n(n));
         launch_multi<CASE>(n, pl, g, pin[q], pout[q], S[q].b[B_F], ctl, k, ka, kb, st, replay);
       } else {
         wave_bands(rows, 128 - 8, resident_waves, ctiles, th, nbands);
@@ -834,8 +857,8 @@ class Solver {
     pb.nb1 = pb.nbe1 = hi_b ? 1 : 0;
     launch_multi<CASE>(n, pb, g, pin, pout, s.b[B_F], ctl, k, ka, kb, st_b);
     if (m > 0) HIPC(hipStreamWaitEvent(st, ev_bnd[pe], 0));
-    const PairPlan pi =
-        multi_plan(g.wj0 + lo_b, g.wj1 + 1 - hi_b, 0, 0, resident_pair_waves - 2 * pb.ctiles, n);
+    const PairPlan pi = multi_plan(g.wj0 + lo_b, g.wj1 + 1 - hi_b, 0, 0, resident_pair_waves - 2 * pb.ctiles, n,
+                                   1 << 30, -1, PAIR_TWC, -1, open_proof_n(n));
     launch_multi<CASE>(n, pi, g, pin, pout, s.b[B_F], ctl, k, ka, kb, st);
     check_launch("poisson (overlapped)");
     HIPC(hipEventRecord(ev_int[e], st));
@@ -1653,17 +1676,23 @@ class Solver {
     if (count != (size_t)(last - first + 1) * cols) throw Error(CFD_E_ARG, "host buffer size does not match field shape");
     const int b = field_buf(field);
     if (chost && b == B_F) srcmax_ready = false;  // a new source from the host
+    // a pressure from the host goes to every p buffer: cells no launch ever
+    // writes (the step block's interior, skipped by the marches) must hold the
+    // same value in each, as the reference's single array holds it
+    const int nb = (chost && field == CFD_FIELD_P) ? nbufs() : 1;
     for (auto& s : S) {
       const int r0 = s.g.wj0, r1 = std::min(s.g.wj1, rows - 1);
       if (r1 < r0) continue;
-      double* dev = s.b[b] + (size_t)(r0 - s.g.row_lo) * pitch;
       const size_t hoff = (size_t)(r0 - first) * cols;
-      if (host)
-        HIPC(hipMemcpy2DAsync(host + hoff, cols * sizeof(double), dev, pitch * sizeof(double), cols * sizeof(double),
-                              r1 - r0 + 1, hipMemcpyDeviceToHost, st));
-      else
-        HIPC(hipMemcpy2DAsync(dev, pitch * sizeof(double), chost + hoff, cols * sizeof(double), cols * sizeof(double),
-                              r1 - r0 + 1, hipMemcpyHostToDevice, st));
+      for (int q = 0; q < nb; ++q) {
+        double* dev = s.b[nb > 1 ? pbuf(q) : b] + (size_t)(r0 - s.g.row_lo) * pitch;
+        if (host)
+          HIPC(hipMemcpy2DAsync(host + hoff, cols * sizeof(double), dev, pitch * sizeof(double), cols * sizeof(double),
+                                r1 - r0 + 1, hipMemcpyDeviceToHost, st));
+        else
+          HIPC(hipMemcpy2DAsync(dev, pitch * sizeof(double), chost + hoff, cols * sizeof(double), cols * sizeof(double),
+                                r1 - r0 + 1, hipMemcpyHostToDevice, st));
+      }
     }
     HIPC(hipStreamSynchronize(st));
   }

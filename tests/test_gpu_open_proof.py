@@ -39,6 +39,9 @@ def run(case, cp, steps, strips=1, **kw):
     ("channel", 400, 96, 3000, 1e-4, 3), ("channel", 700, 300, 400, None, 2), ("channel", 257, 131, 3000, 1e-3, 2),
     ("backwards_step", 400, 100, 3000, 1e-4, 3), ("backwards_step", 900, 260, 300, None, 2),
     ("backwards_step", 517, 131, 2000, 1e-3, 2),
+    # column tiles wholly left of the step's column (step_i = nx/4 >= 3 tiles):
+    # their own class in the plan, interior-column bands below the block
+    ("backwards_step", 1600, 160, 400, None, 2), ("backwards_step", 1800, 200, 3000, 1e-4, 2),
 ])
 def test_open_proof_equals_exact(case, nx, ny, cap, tolf, steps):
     cp = C.make_params(case, nx=nx, ny=ny, max_iters=cap)
@@ -56,13 +59,15 @@ def test_open_proof_equals_exact(case, nx, ny, cap, tolf, steps):
         assert tp.proof_fallbacks >= 1
 
 
-@pytest.mark.parametrize("case", ["channel", "backwards_step"])
+@pytest.mark.parametrize("case,nx,ny", [("channel", 333, 150), ("backwards_step", 333, 150),
+                                        ("backwards_step", 1600, 160)])
 @pytest.mark.parametrize("cap", [37, 40, 41])
-def test_open_proof_vs_red_black_oracle(case, cap):
+def test_open_proof_vs_red_black_oracle(case, nx, ny, cap):
     """One solve from a random source and initial pressure (ghosts included),
     capped inside / at the end of a 4-sweep launch: iteration count, residual
-    (the final field's: proof launches report it from the field) and p."""
-    cp = C.make_params(case, nx=333, ny=150, max_iters=cap)
+    (the final field's: proof launches report it from the field) and p.
+    1600x160: the step's left-of-column tile class (plan nl > 0)."""
+    cp = C.make_params(case, nx=nx, ny=ny, max_iters=cap)
     rng = np.random.default_rng(11)
     f = rng.standard_normal((cp.ny + 2, cp.nx + 2))
     p0 = rng.standard_normal((cp.ny + 2, cp.nx + 2))
@@ -77,12 +82,13 @@ def test_open_proof_vs_red_black_oracle(case, cap):
     g.close()
 
 
-@pytest.mark.parametrize("case", ["channel", "backwards_step"])
+@pytest.mark.parametrize("case,nx", [("channel", 400), ("backwards_step", 400), ("backwards_step", 1600)])
 @pytest.mark.parametrize("strips", [2, 3])
-def test_open_proof_on_strips(case, strips):
+def test_open_proof_on_strips(case, nx, strips):
     """Strips on one device (8-row halos exchanged once per launch: the
-    4-sweep pipeline's depth is 8)."""
-    cp = C.make_params(case, nx=400, ny=240, max_iters=600)
+    4-sweep pipeline's depth is 8). Step 1600 wide: the left-of-column tile
+    class on strips below, across and above the block's lower edge."""
+    cp = C.make_params(case, nx=nx, ny=240, max_iters=600)
     h1, f1, _ = run(case, cp, 2)
     h2, f2, t2 = run(case, cp, 2, strips=strips)
     assert h1 == h2
@@ -97,4 +103,15 @@ def test_open_proof_full_size_channel_capped():
     he, fe, _ = run("channel", cp, 1, proof_test="off")
     assert hp == he
     assert_bits(fp["p"], fe["p"], "channel 4096x512 p")
+    assert tp.proof_fallbacks == 0
+
+
+def test_open_proof_full_size_step_capped():
+    """BASELINE configs[3] (step 8192x512, its left-of-column tile class): a
+    capped step, proof vs exact."""
+    cp = C.make_params("backwards_step", nx=8192, ny=512, max_iters=300)
+    hp, fp, tp = run("backwards_step", cp, 1)
+    he, fe, _ = run("backwards_step", cp, 1, proof_test="off")
+    assert hp == he
+    assert_bits(fp["p"], fe["p"], "step 8192x512 p")
     assert tp.proof_fallbacks == 0
