@@ -832,15 +832,17 @@ struct PairPlan {
   int the, nbe0, nbe1; // boundary column tiles
   int lo0, hi0, lo1, hi1;
   int cxa, cxb;        // step: column tiles across the step's column (+1; 0: none), banded like the boundary ones
-  // step, proof launches (open.hip) only: column tiles 1..nl lie left of the
-  // step's column. Below the block: nlf bands of th rows over [lo0, lz) march
-  // the interior-column path (away from the block edge), nle bands of `the`
-  // rows over [lz, le) the masked one, le = inlet_jmax + 2 (the block's lower
-  // edge row included); then nlt bands of `the` rows over [lt, hi0) when the
-  // range holds ghost row ny + 1 (refreshed from the block's top row). The
-  // block's interior rows between never change (both buffers hold them).
-  // nl = 0: no such class.
-  int nl, nlf, nle, nlt, lz, le, lt;
+  // step, proof launches (open.hip) only: the block's column tiles. Tiles
+  // 1..nl lie left of the step's column, tiles nl+1..nl+ncx cross it (then
+  // cxa = cxb = 0: not boundary-class). Below the block, for both: nlf bands
+  // of th rows over [lo0, lz) march the interior-column path (away from the
+  // block edge), nle bands of `the` rows over [lz, le) the masked one, le =
+  // inlet_jmax + 2 (the block's lower edge row included). Above: the left
+  // tiles' nlt bands of `the` rows over [lt, hi0) when the range holds ghost
+  // row ny + 1 (refreshed from the block's top row; the block's interior rows
+  // between never change, both buffers hold them), the crossing tiles' nxt
+  // bands over [le, hi0) (fluid right of the block). ncx = 0: no such class.
+  int nl, ncx, nlf, nle, nlt, nxt, lz, le, lt;
 };
 
 // column tiles banded as boundary tiles (masked march): the first and last,
@@ -852,7 +854,8 @@ __host__ __device__ inline int plan_edge_tiles(const PairPlan& pl) {
 // waves of a plan (every class)
 __host__ __device__ inline int plan_waves(const PairPlan& pl) {
   const int ne = plan_edge_tiles(pl);
-  return ne * (pl.nbe0 + pl.nbe1) + pl.nl * (pl.nlf + pl.nle + pl.nlt) + (pl.ctiles - ne - pl.nl) * (pl.nb0 + pl.nb1);
+  return ne * (pl.nbe0 + pl.nbe1) + pl.nl * (pl.nlf + pl.nle + pl.nlt) + pl.ncx * (pl.nlf + pl.nle + pl.nxt) +
+         (pl.ctiles - ne - pl.nl - pl.ncx) * (pl.nb0 + pl.nb1);
 }
 
 // PROOF (cavity): the convergence test of each sweep is the proof above

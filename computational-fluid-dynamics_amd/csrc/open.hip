@@ -183,7 +183,7 @@ __device__ __forceinline__ void open_sweeps(const WaveCtx<CASE>& x, const OpenLa
       // row jb (just final for sweep S) into sweep S+1's window, refreshed by
       // its own row and the row reached earlier (lo on the down march)
       double2 v = s.w[S][CFD_SLOT(2 * S + 2)];
-      if (RC)
+      if (RC || EDGE)  // (EDGE without RC: the same-row rules of the ghost columns / block column)
         v = open_refresh<CASE, EDGE, (DIR > 0) ? 1 : 2>(x, L, jb, v, open_lo<DIR, ROT>(s.w[S], 2 * S + 2),
                                                         open_hi<DIR, ROT>(s.w[S], 2 * S + 2));
       s.w[S + 1][CFD_SLOT(2 * S + 2)] = v;
@@ -209,7 +209,7 @@ __device__ __forceinline__ void open_sweeps(const WaveCtx<CASE>& x, const OpenLa
       const int js = R - (2 * S + 3) * DIR;
       if (js >= x.y0 && js < x.y1 && x.out_lane) {
         double2 v = s.w[S][CFD_SLOT(2 * S + 3)];
-        if (RC)
+        if (RC || EDGE)
           v = open_refresh<CASE, EDGE, 3>(x, L, js, v, open_lo<DIR, ROT>(s.w[S], 2 * S + 3),
                                           open_hi<DIR, ROT>(s.w[S], 2 * S + 3));
         store_row_pair(x.pout, x.prs, (size_t)(js - x.g.row_lo) * (size_t)x.g.pitch + x.gi, v);
@@ -241,9 +241,15 @@ __device__ __forceinline__ void open_step(const WaveCtx<CASE>& x, const OpenLane
 }
 
 // one wave's band [y0, y1): dm[q] = max |black update| of sweep q over its
-// proving output cells (interior-column waves; 0 on EDGE waves), pm = max |p_in|
+// proving output cells (interior-column waves; 0 on EDGE waves), pm = max |p_in|.
+// RC: each group of 10 steps whose rows (the front's 10 rows, the pipeline
+// behind them and their neighbours) all lie in (gmin, gmax) - no ghost row,
+// no row outside the stored ones, for the step's block columns nothing at or
+// above the block's lower edge - runs without row checks or row rules (RC
+// false: the same instructions as an interior band), the others with them.
 template <int NS, int CASE, int DIR, bool EDGE, bool RC>
-__device__ __forceinline__ void open_march(const WaveCtx<CASE>& x, int y0, int y1, double (&dm)[NS], double& pm) {
+__device__ __forceinline__ void open_march(const WaveCtx<CASE>& x, int y0, int y1, double (&dm)[NS], double& pm,
+                                           int gmin = 0, int gmax = 0) {
   constexpr int H = 2 * NS + 1, PD = OPEN_PD;
   const int Rb0 = (DIR > 0) ? y0 - H : y1 - 1 + H;
   const int Rbeg = Rb0 - DIR * (Rb0 & 1);  // even first front row: compile-time colours
@@ -269,7 +275,22 @@ __device__ __forceinline__ void open_march(const WaveCtx<CASE>& x, int y0, int y
     }
   }
   int R = Rbeg;
+  constexpr int BACK = 2 * NS + 5;  // rows behind the front a step touches (store row + neighbour + 1)
   for (int st = 0; st < nsteps; st += 10, R += 10 * DIR) {
+    const int glo = (DIR > 0) ? R - BACK : R - 11, ghi = (DIR > 0) ? R + 11 : R + BACK;
+    if (RC && glo > gmin && ghi < gmax) {  // (wave-uniform)
+      open_step<NS, CASE, DIR, 0, 0, EDGE, false>(x, L, s, R);
+      open_step<NS, CASE, DIR, 1, 1, EDGE, false>(x, L, s, R + DIR);
+      open_step<NS, CASE, DIR, 2, 0, EDGE, false>(x, L, s, R + 2 * DIR);
+      open_step<NS, CASE, DIR, 3, 1, EDGE, false>(x, L, s, R + 3 * DIR);
+      open_step<NS, CASE, DIR, 4, 0, EDGE, false>(x, L, s, R + 4 * DIR);
+      open_step<NS, CASE, DIR, 0, 1, EDGE, false>(x, L, s, R + 5 * DIR);
+      open_step<NS, CASE, DIR, 1, 0, EDGE, false>(x, L, s, R + 6 * DIR);
+      open_step<NS, CASE, DIR, 2, 1, EDGE, false>(x, L, s, R + 7 * DIR);
+      open_step<NS, CASE, DIR, 3, 0, EDGE, false>(x, L, s, R + 8 * DIR);
+      open_step<NS, CASE, DIR, 4, 1, EDGE, false>(x, L, s, R + 9 * DIR);
+      continue;
+    }
     open_step<NS, CASE, DIR, 0, 0, EDGE, RC>(x, L, s, R);
     open_step<NS, CASE, DIR, 1, 1, EDGE, RC>(x, L, s, R + DIR);
     open_step<NS, CASE, DIR, 2, 0, EDGE, RC>(x, L, s, R + 2 * DIR);
@@ -327,6 +348,7 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
   const int ne = (pl.ctiles >= 2) ? 2 : 1;
   const int ned = plan_edge_tiles(pl);
   const int nbe = pl.nbe0 + pl.nbe1, nbi = pl.nb0 + pl.nb1, nlb = pl.nlf + pl.nle + pl.nlt;
+  const int nxb = pl.nlf + pl.nle + pl.nxt;
   int band, ctile, y0, y1;
   // band `band` of a class with bands of th rows: nb0 of them over [lo0, hi0), then [lo1, hi1)
   auto rows_of = [&](int th, int nb0) {
@@ -339,25 +361,27 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
     ctile = (e == 0) ? 0 : (e == 1 && ne == 2) ? pl.ctiles - 1 : (e == ne && pl.cxa > 0) ? pl.cxa - 1 : pl.cxb - 1;
     band = tile % nbe;
     rows_of(pl.the, pl.nbe0);
-  } else if (tile < ned * nbe + pl.nl * nlb) {  // step: left of the step's column
-    const int t = tile - ned * nbe;
-    ctile = 1 + t % pl.nl;
-    band = t / pl.nl;
-    if (band < pl.nlf) {
+  } else if (tile < ned * nbe + pl.nl * nlb + pl.ncx * nxb) {  // step: the block's column tiles
+    const bool left = tile < ned * nbe + pl.nl * nlb;
+    const int t = left ? tile - ned * nbe : tile - ned * nbe - pl.nl * nlb;
+    const int nt = left ? pl.nl : pl.ncx;
+    ctile = 1 + (left ? 0 : pl.nl) + t % nt;
+    band = t / nt;
+    if (band < pl.nlf) {  // below the block's edge zone: interior path
       y0 = pl.lo0 + band * pl.th;
       y1 = min(y0 + pl.th, pl.lz);
-    } else if (band < pl.nlf + pl.nle) {
+    } else if (band < pl.nlf + pl.nle) {  // the edge zone
       y0 = pl.lz + (band - pl.nlf) * pl.the;
       y1 = min(y0 + pl.the, pl.le);
-    } else {
-      y0 = pl.lt + (band - pl.nlf - pl.nle) * pl.the;
+    } else {  // above: ghost row ny + 1 (left) / the fluid right of the block (crossing)
+      y0 = (left ? pl.lt : pl.le) + (band - pl.nlf - pl.nle) * pl.the;
       y1 = min(y0 + pl.the, pl.hi0);
     }
   } else {
-    const int t = tile - ned * nbe - pl.nl * nlb;
-    const int nci = pl.ctiles - ned - pl.nl;
+    const int t = tile - ned * nbe - pl.nl * nlb - pl.ncx * nxb;
+    const int nci = pl.ctiles - ned - pl.nl - pl.ncx;
     if (t >= nci * nbi) return;
-    ctile = 1 + pl.nl + t % nci;
+    ctile = 1 + pl.nl + pl.ncx + t % nci;
     band = t / nci;
     if (pl.cxa > 0 && ctile >= pl.cxa - 1) ++ctile;
     if (pl.cxb > 0 && ctile >= pl.cxb - 1) ++ctile;
@@ -386,12 +410,11 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
   const int c0 = ctile * PAIR_TWC - H;
   constexpr int CONE = 2 * NS + 2;  // rows the march reads beyond its band (pipeline + parity row)
   // interior-column wave: every column a fluid cell with fluid neighbours, off
-  // the step's block: right of the block, or left of the step's column with
-  // every row the march reads below the block's lower edge row (inlet_jmax +
-  // 1, refreshed each sweep: the margin mirrors `safe`'s for ghost row ny + 1)
+  // the step's block: right of the block, or every row the march reads below
+  // the block's lower edge row (inlet_jmax + 1, refreshed each sweep: the
+  // margin mirrors `safe`'s for ghost row ny + 1)
   const bool cols_in = c0 >= 1 && c0 + 127 <= g.nx &&
-                       (CASE != BACKSTEP || c0 > c.step_i + 1 ||
-                        (c0 + 127 <= c.step_i - 1 && y1 + CONE < c.inlet_jmax + 1));
+                       (CASE != BACKSTEP || c0 > c.step_i + 1 || y1 + CONE < c.inlet_jmax + 1);
   if (CASE == BACKSTEP && c0 >= 1 && c0 + 127 <= c.step_i - 1 && y0 - CONE >= c.inlet_jmax + 2 &&
       y1 + CONE <= g.ny) {
     // a band inside the block, away from fluid and ghost rows / columns:
@@ -407,11 +430,15 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0_)::"memory");
 #endif
   double dm[NS], pm = 0.0;
-  if (!cols_in) open_march<NS, CASE, 1, true, true>(x, y0, y1, dm, pm);
+  // rows of the groups that may run without row checks: (gmin, gmax)
+  const int gmin = x.rmin;
+  int gmax = min(x.rmax, g.ny + 1);
+  if (CASE == BACKSTEP && c0 <= c.step_i + 1) gmax = min(gmax, c.inlet_jmax);
+  if (!cols_in) open_march<NS, CASE, 1, true, true>(x, y0, y1, dm, pm, gmin, gmax);
   else if (safe && up) open_march<NS, CASE, -1, false, false>(x, y0, y1, dm, pm);
   else if (safe) open_march<NS, CASE, 1, false, false>(x, y0, y1, dm, pm);
-  else if (up) open_march<NS, CASE, -1, false, true>(x, y0, y1, dm, pm);
-  else open_march<NS, CASE, 1, false, true>(x, y0, y1, dm, pm);
+  else if (up) open_march<NS, CASE, -1, false, true>(x, y0, y1, dm, pm, gmin, gmax);
+  else open_march<NS, CASE, 1, false, true>(x, y0, y1, dm, pm, gmin, gmax);
   double growth = 1.0;
 #pragma unroll
   for (int q = 0; q < NS; ++q) growth *= 9.0;

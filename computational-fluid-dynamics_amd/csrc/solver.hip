@@ -141,9 +141,11 @@ class Solver {
     return P.case_id == CFD_CAVITY ? 3 : 2;
   }
   // LDS-tile launches (tile.hpp): red-black, one strip, no ranks, a grid of at
-  // most tile_rounds resident rounds of tiles (CFD_TUNE_TILE_ROUNDS)
+  // most tile_rounds resident rounds of tiles (CFD_TUNE_TILE_ROUNDS). Default:
+  // 1 for the cavity, 0 for the open cases (their wave march with unchecked
+  // row groups is faster: channel 4096x512 8.2 us per sweep against 9.9)
   bool tile_on = false;
-  int tile_rounds = 1;
+  int tile_rounds = 1;  // (open cases: 0, set in init)
   TilePlan tplan{};
   void plan_tiles() {
     tile_on = false;
@@ -299,6 +301,8 @@ class Solver {
         // DESIGN.md §4)
         pair_edge_pct = 80;
         if (proof_ok()) pps = std::min(pps, 2);
+      } else {
+        tile_rounds = 0;
       }
       if (use_lexw()) {
         int lps = 0;
@@ -661,9 +665,10 @@ class Solver {
   // rows, marched in groups of 10 over th + march_extra rows, so th + extra is
   // a multiple of 10. The two boundary column tiles march slower (masks):
   // shorter bands, pair_edge_pct % of the interior march.
-  // left_class (the step's proof launches, open.hip): the column tiles left of
-  // the step's column become their own class (PairPlan::nl), banded over the
-  // rows below the block only, with short bands next to its lower edge.
+  // left_class (the step's proof launches, open.hip): the column tiles over
+  // the step's block (left of its column and across it) become their own
+  // class (PairPlan::nl / ncx): interior-path bands below the block, short
+  // masked bands next to its lower edge and above it.
   PairPlan multi_plan(int lo0, int hi0, int lo1, int hi1, int waves, int n, int max_th = 1 << 30,
                       int edge_pct = -1, int twc = PAIR_TWC, int ex = -1, bool left_class = false) const {
     if (edge_pct < 0) edge_pct = pair_edge_pct;
@@ -687,12 +692,17 @@ class Solver {
     const int rmax = std::max(hi0 - lo0, hi1 - lo1);
     if (ex < 0) ex = march_extra(n);
     auto nbands = [](int lo, int hi, int t) { return hi > lo ? (hi - lo + t - 1) / t : 0; };
-    // the left class: column tiles 1 .. cxa-2 (wholly left of the step's
-    // column); rows [lo0, lz) interior-column bands (every row the march
-    // reads below the block's lower edge row: open.hip cols_in), [lz, le) short
-    const bool lc = left_class && P.case_id == CFD_BACKSTEP && pl.cxa > 2 && hi1 <= lo1;
+    // the block's column class (PairPlan::nl / ncx): column tiles 1 .. cxa-2
+    // (wholly left of the step's column) and the crossing ones; rows [lo0, lz)
+    // interior-column bands (every row the march reads below the block's
+    // lower edge row: open.hip cols_in), [lz, le) short masked bands, above
+    // that the top ghost row (left tiles) or every row (crossing tiles)
+    const int cx_last = pl.cxb > 0 ? pl.cxb - 1 : pl.cxa - 1;  // the last crossing tile
+    const bool lc = left_class && P.case_id == CFD_BACKSTEP && pl.cxa > 1 && cx_last < pl.ctiles - 1 && hi1 <= lo1;
     if (lc) {
       pl.nl = pl.cxa - 2;
+      pl.ncx = pl.cxb > 0 ? 2 : 1;
+      pl.cxa = pl.cxb = 0;  // (the crossing tiles leave the boundary class)
       pl.lz = std::max(lo0, std::min(hi0, C.inlet_jmax - (2 * n + 2)));
       pl.le = std::max(pl.lz, std::min(hi0, C.inlet_jmax + 2));
       pl.lt = hi0;  // (ghost row ny + 1 in the range: set with `the` below)
@@ -703,6 +713,7 @@ class Solver {
       pl.nle = nbands(pl.lz, pl.le, pl.the);
       if (hi0 == P.ny + 2) pl.lt = std::max(pl.le, hi0 - pl.the);
       pl.nlt = nbands(pl.lt, hi0, pl.the);
+      pl.nxt = nbands(pl.le, hi0, pl.the);
     };
     int nb = std::max(1, std::min(waves / std::max(1, pl.ctiles), (rows + march_min_th - 1) / march_min_th));
     nb = std::max(nb, (rows + max_th - 1) / max_th);
