@@ -863,6 +863,16 @@ __host__ __device__ inline int plan_waves(const PairPlan& pl) {
 #ifndef CFD_PROOF_MIN_WAVES
 #define CFD_PROOF_MIN_WAVES 2  // proof-mode launches are planned for 2 waves per SIMD (Solver::init)
 #endif
+// diagnostic build only (CFD_MARCH_STAMPS=1, never the product library): each
+// wave's march cycles with its tile, band and path (solver.hip cfd_march_stamps)
+#ifndef CFD_MARCH_STAMPS
+#define CFD_MARCH_STAMPS 0
+#endif
+#if CFD_MARCH_STAMPS
+constexpr int MARCH_STAMP_MAX = 8192;
+static __device__ long long march_stamp_buf[MARCH_STAMP_MAX * 8];
+#endif
+
 template <int CASE, int NS, bool PROOF = false>
 __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY) ? CFD_CAV_MIN_WAVES : CFD_PAIR_MIN_WAVES) void poisson_multi_kernel(
     Geo g, Coef c, const double* __restrict__ pin, double* __restrict__ pout, const double* __restrict__ f,
@@ -969,6 +979,10 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
   // no row checks (cav_update RC)
   const bool safe = y0 - (2 * NS + 2) > x.rmin && y1 + (2 * NS + 2) < min(x.rmax, g.ny);
   const bool fast = cols_in;
+#if CFD_MARCH_STAMPS
+  long long t0_;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0_)::"memory");
+#endif
   double r[NS];
   if constexpr (CASE == CAVITY) {  // the cavity's own pipeline (no refresh stage: depth 2NS+1)
     if constexpr (PROOF) {
@@ -1019,6 +1033,19 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
                 (unsigned long long)__double_as_longlong(r[q]));
     }
   }
+#if CFD_MARCH_STAMPS
+  {
+    long long t1_;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_)::"memory");
+    if (tile < MARCH_STAMP_MAX && lane < 8) {
+      const long long v[8] = {tile, ctile, band, y0, y1, fast ? 1 : 0, safe ? 1 : 0, t1_ - t0_};
+      long long o = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o = lane == q ? v[q] : o;
+      march_stamp_buf[(size_t)tile * 8 + lane] = o;
+    }
+  }
+#endif
 }
 
 }  // namespace cfd

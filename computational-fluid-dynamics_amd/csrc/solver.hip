@@ -1847,6 +1847,16 @@ int cfd_get_field(cfd_solver* s, int field, double* host, size_t count) {
   });
 }
 
+#if CFD_MARCH_STAMPS
+// diagnostic build only: per wave {tile, column tile, band, y0, y1, interior
+// columns, safe, cycles} of the last poisson_multi_kernel launch
+extern "C" int cfd_march_stamps(long long* out, int n) {
+  if (n > cfd::MARCH_STAMP_MAX * 8) n = cfd::MARCH_STAMP_MAX * 8;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cfd::march_stamp_buf), (size_t)n * 8) == hipSuccess ? n : -1;
+}
+#endif
+
 int cfd_set_field(cfd_solver* s, int field, const double* host, size_t count) {
   return guard([&] {
     if (!host) throw Error(CFD_E_ARG, "null host buffer");

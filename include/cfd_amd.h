@@ -212,7 +212,8 @@ enum cfd_tuning {
   CFD_TUNE_TENT_TH = 6,       /* rows per band of the predictor's march (>= 4) */
   CFD_TUNE_LEXW_RAMP_PCT = 7, /* lexicographic ramp launches: band height floor, % of the steady plan's (0..100) */
   CFD_TUNE_TILE_ROUNDS = 8    /* red-black, one strip: LDS-tile launches when the grid fits this many
-                                 resident rounds of tiles (one per CU; 0: never, the march launches) */
+                                 resident rounds of tiles (one per CU; 0: never, the march launches;
+                                 default 1 for the cavity, 0 for the open cases) */
 };
 int cfd_set_tuning(cfd_solver* s, int knob, int value);
 

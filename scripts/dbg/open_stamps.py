@@ -4,6 +4,8 @@ last launch's waves grouped by path (interior columns / safe band / edge
 masks) and column class (left of the step's column, across it, right).
 
 usage: CFD_AMD_LIB=libcfd_amd_ostamps.so python3 scripts/dbg/open_stamps.py case nx ny [max_iters]
+(CFD_STAMPS_FN=cfd_march_stamps with a CFD_MARCH_STAMPS=1 build: the cavity /
+pair march, poisson_multi_kernel)
 """
 import collections
 import ctypes
@@ -25,7 +27,7 @@ s.synchronize()
 L = _lib.lib()
 n = 8192 * 8
 buf = (ctypes.c_longlong * n)()
-L.cfd_open_stamps(buf, n)
+getattr(L, os.environ.get("CFD_STAMPS_FN", "cfd_open_stamps"))(buf, n)
 a = np.frombuffer(buf, dtype=np.int64).reshape(8192, 8)
 a = a[a[:, 7] > 0]
 step_i = getattr(cp, "step_i", 0) if case == "backwards_step" else -1
