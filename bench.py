@@ -181,7 +181,7 @@ def kcase_of(case: str) -> str:
     return "cavity" if case == "rayleigh_benard" else case  # Rayleigh-Benard runs the cavity SOR kernels
 
 
-def main() -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -198,16 +198,19 @@ def main() -> int:
     ap.add_argument("--check-every", type=int, default=1,
                     help="residual test every N SOR iterations (1 = the reference's stop rule, at every GPU count)")
     ap.add_argument("--sweeps-per-launch", type=int, default=0,
-                    help="SOR iterations fused per kernel launch (0: auto = 4 for the red-black cavity's "
-                         "proof-mode launches, 3 for exact-residual ones, 2 for the open cases)")
+                    help="SOR iterations fused per kernel launch (0: auto = 4 in red-black proof-mode launches - "
+                         "3 for the backwards step on ranks -, 3 (cavity) / 2 (open cases) with exact residuals; "
+                         "4 in the reference's order, 3 on strips)")
     ap.add_argument("--proof-test", default="auto", choices=["auto", "off"],
-                    help="red-black cavity: proof-mode convergence test (off: exact residual every sweep)")
+                    help="red-black launches (every case): proof-mode convergence test (off: exact residual every "
+                         "sweep)")
     ap.add_argument("--ordering", default="rb", choices=["rb", "lex"],
-                    help="SOR sweep order: rb (red-black) or lex (the reference's lexicographic order, bit-identical)")
+                    help="SOR sweep order of the headline: rb (red-black: splits over GPUs) or lex (the reference's "
+                         "lexicographic order, bit-identical; one GPU)")
     ap.add_argument("--lex-sweeps", type=int, default=0,
                     help="reference_order: sweeps per lexicographic-order launch (0: auto = 4; 5 for the cavity)")
     ap.add_argument("--lex-steps", type=int, default=2,
-                    help="N=1 cavity: also time this many steps in the reference's own (lexicographic) order "
+                    help="N=1: also time this many steps in the reference's own (lexicographic) order "
                          "(0: skip); reported as reference_order")
     ap.add_argument("--tile-rounds", type=int, default=-1,
                     help="red-black, one GPU: LDS-tile SOR launches when the grid fits this many resident rounds of "
@@ -216,24 +219,81 @@ def main() -> int:
                     help="launch-planning knob (cfd_amd._lib.TUNING names; performance only, same bits)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--loopback-ranks", type=int, default=0,
+                    help="test mode: run the multi-rank code path with this many ranks as host threads sharing "
+                         "GPU 0 over the library's loopback transport (no RCCL; timings are not a measurement)")
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    n_gpus = world
 
-    import torch  # noqa: E402  (first: PyTorch's HIP runtime is the one the library binds to)
-    import torch.distributed as dist
+class TorchGroup:
+    """Barrier / max / sum over the ranks of the torch.distributed group (gloo:
+    host scalars only; the data path's halos and residuals travel over RCCL
+    inside the library)."""
+
+    def __init__(self, dist, world: int):
+        self.dist, self.world = dist, world
+
+    def barrier(self) -> None:
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, v: float) -> float:
+        from cfd_amd.dist import max_over_ranks
+        return max_over_ranks(self.dist, v) if self.world > 1 else v
+
+    def sum(self, v: float) -> float:
+        from cfd_amd.dist import sum_over_ranks
+        return sum_over_ranks(self.dist, v) if self.world > 1 else v
+
+
+class ThreadGroup:
+    """The same three operations for ranks that are host threads of one
+    process (--loopback-ranks)."""
+
+    def __init__(self, world: int):
+        import threading
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.vals = [0.0] * world
+        self.rank_of = {}
+
+    def barrier(self) -> None:
+        self.bar.wait(timeout=600)
+
+    def _reduce(self, rank: int, v: float, op) -> float:
+        self.barrier()
+        self.vals[rank] = float(v)
+        self.barrier()
+        out = op(self.vals)
+        self.barrier()
+        return out
+
+    def bind(self, rank: int) -> "ThreadGroup._Bound":
+        return ThreadGroup._Bound(self, rank)
+
+    class _Bound:
+        def __init__(self, g, rank):
+            self.g, self.rank = g, rank
+
+        def barrier(self) -> None:
+            self.g.barrier()
+
+        def max(self, v: float) -> float:
+            return self.g._reduce(self.rank, v, max)
+
+        def sum(self, v: float) -> float:
+            return self.g._reduce(self.rank, v, lambda xs: float(sum(xs)))
+
+
+def run(args, rank: int, world: int, local_rank: int, comm, group, loopback: bool = False) -> dict | None:
+    """One rank's benchmark: build the solver for its rows, W untimed warmup
+    steps, then K timed steps bracketed by a barrier and device syncs on both
+    sides; the elapsed time is the max over ranks and the cell updates the sum.
+    Returns rank 0's JSON line (None on the other ranks)."""
+    import torch
 
     import cfd_amd as C
     from cfd_amd import _lib
-
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     check_every = max(1, args.check_every)
     strong = args.global_ny > 0
@@ -246,25 +306,21 @@ def main() -> int:
     for kv in args.tune:
         k_, v_ = kv.split("=", 1)
         tuning[k_] = int(v_)
-    comm = None
     comm_info = None
     if world > 1:
         from cfd_amd.dist import comm_info as _comm_info
-        from cfd_amd.dist import init_comm, strip_rows, weak_rows
-        comm = init_comm(dist, rank, world, local_rank)
+        from cfd_amd.dist import strip_rows, weak_rows
         comm_info = _comm_info(comm)
         rows = strip_rows(rank, world, ny_global) if strong else weak_rows(rank, args.ny)
+        if args.ordering != "rb":
+            raise SystemExit("the reference's order runs on one GPU (DESIGN.md §5): use --ordering rb with N > 1")
         solver = C.solver_for(cp, device=local_rank, check_every=check_every, rank_rows=rows, comm=comm,
                               sweeps_per_launch=args.sweeps_per_launch, ordering=args.ordering,
-                              proof_test=args.proof_test)
+                              proof_test=args.proof_test, tuning=tuning)
     else:
         solver = C.solver_for(cp, device=local_rank, check_every=check_every,
                               sweeps_per_launch=args.sweeps_per_launch, ordering=args.ordering,
                               proof_test=args.proof_test, tuning=tuning)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
 
     if args.case == "cavity":  # cavity-01.cpp:380 (the open cases apply their BCs in the constructor)
         solver.applyBoundaryConditions()
@@ -273,7 +329,7 @@ def main() -> int:
     solver.synchronize()
     solver.reset_timing()
 
-    barrier()
+    group.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     iters, resids = [], []
@@ -283,21 +339,22 @@ def main() -> int:
         resids.append(res)
     solver.synchronize()
     torch.cuda.synchronize()
-    barrier()
+    group.barrier()
     elapsed = time.perf_counter() - t0
     tm = solver.timing()
 
     updates = float(tm.poisson_cell_updates)
-    if world > 1:
-        from cfd_amd.dist import max_over_ranks, sum_over_ranks
-        elapsed = max_over_ranks(dist, elapsed)
-        updates = sum_over_ranks(dist, updates)
+    elapsed = group.max(elapsed)
+    updates = group.sum(updates)
+    n_gpus = world
 
+    line = None
     if rank == 0:
         g0, g1 = solver.owned_rows()
         wrows = (g1 - g0 + 1) + (1 if g0 == 1 else 0) + (1 if g1 == cp.ny else 0)
         cells_per_launch = wrows * (cp.nx + 2)
-        lexw = args.ordering == "lex" and kcase_of(args.case) in ("cavity", "channel")
+        sor_kernel = _lib.SOR_KERNEL.get(tm.sor_kernel, "?")
+        lexw = sor_kernel == "lexw"
         if lexw and tm.poisson_steady_launches > 0:
             # lexicographic order: the launches with every cell active (the
             # ramps at both ends of a solve skip or mask part of the grid)
@@ -316,10 +373,9 @@ def main() -> int:
                               round(sweeps_per_launch))
         mlups = updates / elapsed / 1e6
         kcase = kcase_of(args.case)
-        # red-black cavity launches: proof-mode convergence test (DESIGN.md
-        # §2; --proof-test off evaluates the residual in every sweep)
-        sor_kernel = _lib.SOR_KERNEL.get(tm.sor_kernel, "?")
-        proof = (not lexw and args.proof_test != "off"
+        # red-black launches: proof-mode convergence test (DESIGN.md §2;
+        # --proof-test off evaluates the residual in every sweep)
+        proof = (args.ordering == "rb" and args.proof_test != "off"
                  and (sor_kernel == "tile" or (sor_kernel == "march" and round(sweeps_per_launch) >= 3)))
         rows_here = g1 - g0 + 1
         per_gpu = (f"{cp.nx}x{rows_here} fp64 cells per GPU (global {cp.nx}x{cp.ny} split over {n_gpus} GPUs)"
@@ -349,6 +405,8 @@ def main() -> int:
             "rccl_ranks": comm_info["nranks"] if comm_info else None,
             "transport": (comm_info["transport"] if comm_info else "none (1 GPU)"),
             "steps_per_sec": round(args.steps / elapsed, 4),
+            "elapsed_s": round(elapsed, 6),
+            "poisson_cell_updates": int(updates),
             "sor_iterations_per_step": iters,
             "sor_cap_hits": sum(1 for i in iters if i >= cp.max_iters),
             "final_residual_per_step": [float(f"{r:.6e}") for r in resids],
@@ -368,7 +426,8 @@ def main() -> int:
                            else f"poisson_open_proof_kernel<{kcase},{round(sweeps_per_launch)}>" if proof
                            else f"poisson_multi_kernel<{kcase},3>" if sweeps_per_launch > 2.5
                            else f"poisson_multi_kernel<{kcase},2>" if sweeps_per_launch > 1.5
-                           else f"poisson_wave_kernel<{kcase}>"),
+                           else f"poisson_wave_kernel<{kcase}>" if sor_kernel == "march"
+                           else f"{sor_kernel} ({kcase}, whole solve in one launch)"),
                 "bytes_per_launch": BYTES_PER_CELL * cells_per_launch,
                 "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "sweeps_per_launch": round(sweeps_per_launch, 4),
@@ -376,19 +435,84 @@ def main() -> int:
                 "effective_sweep_frac": round(effective / HBM_PEAK_GBS, 4),
             },
         }
+        if loopback:
+            line["config"]["loopback_ranks_on_one_gpu"] = world
         if not args.no_cpu_baseline and world == 1:  # the CPU leg is timed at N=1 only
             log("timing the CPU baseline ...")
             line["cpu_baseline"] = cpu_baseline(cp.nx, cp.ny, args.cpu_seconds, args.case)
             if args.case == "cavity":  # beside it: the reference's own binary on its own case (same host)
                 line["cpu_baseline"]["reference_binary"] = reference_binary()
+        if world == 1 and args.lex_steps > 0 and args.ordering == "rb" and args.case != "rayleigh_benard":
+            line["reference_order"] = reference_order(C, cp, args, local_rank, check_every, cells_per_launch)
+    solver.close()
+    return line
 
-    if (rank == 0 and world == 1 and args.lex_steps > 0 and args.ordering == "rb"
-            and kcase_of(args.case) in ("cavity", "channel")):
-        line["reference_order"] = reference_order(C, cp, args, local_rank, check_every, cells_per_launch)
+
+def run_loopback(args) -> dict:
+    """--loopback-ranks N: the rank path of run() with N host-thread ranks on
+    GPU 0 (cfd_comm_init_loopback: the same group send / recv / all-reduce
+    call sites as RCCL), for tests/test_gpu_bench_ranks.py."""
+    import threading
+
+    import torch  # noqa: F401  (first: PyTorch's HIP runtime is the one the library binds to)
+
+    from cfd_amd import _lib
+
+    world = args.loopback_ranks
+    L = _lib.lib()
+    hub = L.cfd_comm_loopback_hub(world)
+    group = ThreadGroup(world)
+    out, errors = [None], []
+
+    def body(r):
+        try:
+            comm = L.cfd_comm_init_loopback(hub, r, 0)
+            if not comm:
+                raise _lib.CfdError(L.cfd_last_error().decode())
+            line = run(args, r, world, 0, comm, group.bind(r), loopback=True)
+            if r == 0:
+                out[0] = line
+            L.cfd_comm_destroy(comm)
+        except BaseException as e:  # noqa: BLE001
+            errors.append(e)
+            group.bar.abort()
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    L.cfd_comm_loopback_hub_destroy(hub)
+    if errors:
+        raise errors[0]
+    return out[0]
+
+
+def main() -> int:
+    args = parse_args()
+    if args.loopback_ranks > 0:
+        print(json.dumps(run_loopback(args)), flush=True)
+        return 0
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+
+    import torch  # noqa: E402  (first: PyTorch's HIP runtime is the one the library binds to)
+    import torch.distributed as dist
+
+    from cfd_amd import _lib
+
+    torch.cuda.set_device(local_rank)
+    comm = None
+    if world > 1:
+        from cfd_amd.dist import init_comm
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        comm = init_comm(dist, rank, world, local_rank)
+    line = run(args, rank, world, local_rank, comm, TorchGroup(dist, world))
     if rank == 0:
         print(json.dumps(line), flush=True)
-
-    solver.close()
     if comm:
         _lib.lib().cfd_comm_destroy(comm)
     if world > 1:

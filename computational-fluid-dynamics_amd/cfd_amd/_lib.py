@@ -48,7 +48,7 @@ ORDER = {"rb": 0, "lex": 1}
 SWITCH = {"auto": 0, "on": 1, "off": 2}  # enum cfd_switch
 TUNING = {"pair_wps": 0, "wave_wps": 1, "lexw_waves": 2, "lexw_edge_pct": 3, "pair_edge_pct": 4,
           "march_min_th": 5, "tent_th": 6, "lexw_ramp_pct": 7, "tile_rounds": 8}  # enum cfd_tuning
-SOR_KERNEL = {0: "none", 1: "march", 2: "tile", 3: "small", 4: "lexw", 5: "lex"}  # enum cfd_sor_kernel
+SOR_KERNEL = {0: "none", 1: "march", 2: "tile", 3: "small", 4: "lexw", 5: "lex", 6: "smlex"}  # enum cfd_sor_kernel
 
 
 class StepInfo(ctypes.Structure):
@@ -101,6 +101,7 @@ SIGNATURES = {
     "cfd_reset_timing": (_i, [_vp]),
     "cfd_synchronize": (_i, [_vp]),
     "cfd_set_tuning": (_i, [_vp, _i, _i]),
+    "cfd_tuning_default": (_i, [ctypes.POINTER(CfdParams), _i, _ip]),
     "cfd_comm_unique_id": (_i, [ctypes.POINTER(ctypes.c_ubyte)]),
     "cfd_comm_init": (_vp, [ctypes.POINTER(ctypes.c_ubyte), _i, _i, _i]),
     "cfd_comm_destroy": (_i, [_vp]),

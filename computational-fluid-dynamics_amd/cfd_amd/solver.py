@@ -19,7 +19,7 @@ from .logfmt import step_line, warning_line
 from .params import BACKSTEP, CASE_NAMES, CAVITY, CHANNEL, RAYLEIGH_BENARD, CaseParams, make_params
 
 
-def to_cparams(cp: CaseParams, check_every: int = 1, chunk: int = 0, ordering: str = "rb",
+def to_cparams(cp: CaseParams, check_every: int = 1, chunk: int = 0, ordering: str = "lex",
                sweeps_per_launch: int = 0, proof_test: str = "auto", small_solve: str = "auto",
                overlap: str = "auto") -> _lib.CfdParams:
     """Derived reference constants -> the C-ABI parameter block. proof_test /
@@ -40,18 +40,23 @@ class _SolverBase:
 
     def __init__(self, params: CaseParams | None = None, *, device: int = 0, n_strips: int = 1,
                  check_every: int = 1, chunk: int = 0, rank_rows: tuple[int, int] | None = None, comm=None,
-                 ordering: str = "rb", sweeps_per_launch: int = 0, proof_test: str = "auto",
+                 ordering: str = "auto", sweeps_per_launch: int = 0, proof_test: str = "auto",
                  small_solve: str = "auto", overlap: str = "auto", tuning: dict[str, int] | None = None):
-        """ordering: "rb" (red-black SOR, the fast default) or "lex" (the reference's
-        lexicographic sweep, bit-identical to it; one device).
+        """ordering: "lex" (the reference's lexicographic sweep, bit-identical to the
+        reference binaries: the default on one device, strips allowed), "rb" (red-black
+        SOR: the rank path, required with rank_rows) or "auto" (lex on one device, rb
+        on ranks; Rayleigh-Benard, which has no reference solver: rb).
         sweeps_per_launch: SOR iterations fused per kernel launch (0 = auto: red-black
-        cavity 4 in proof-mode launches and 3 in exact ones, 2 for the open cases;
-        lexicographic 3); bit-identical either way.
+        4 in proof-mode launches (the step on strips or ranks: 3), 3 (cavity) / 2 (open
+        cases) in exact ones; lexicographic 4, 3 on strips); bit-identical either way.
         proof_test / small_solve / overlap: "auto" / "on" / "off" (include/cfd_amd.h).
         tuning: launch-planning knobs (_lib.TUNING names), performance only."""
         self.params = params if params is not None else make_params(self.CASE)
         if self.params.case_id != self.CASE:
             raise ValueError(f"{type(self).__name__} needs case {CASE_NAMES[self.CASE]}")
+        if ordering == "auto":
+            ordering = "rb" if (rank_rows is not None or self.CASE == RAYLEIGH_BENARD) else "lex"
+        self.ordering = ordering
         self._cp = to_cparams(self.params, check_every, chunk, ordering, sweeps_per_launch, proof_test,
                               small_solve, overlap)
         L = _lib.lib()

@@ -33,7 +33,9 @@ extern "C" int cfd_params_init(int case_id, double re, int nx, int ny, double dt
   p.case_id = case_id;
   p.check_every = 1;
   p.chunk = 0;
-  p.ordering = CFD_ORDER_RB;
+  // the reference's own sweep order (bit-identical output) on one device; the
+  // rank path (cfd_create_rank) needs CFD_ORDER_RB
+  p.ordering = CFD_ORDER_LEX;
   p.sweeps_per_launch = 0;
   switch (case_id) {
     case CFD_CAVITY:
@@ -110,7 +112,7 @@ extern "C" int cfd_params_init_rb(double ra, double pr, int nx, int ny, double d
   std::memset(&p, 0, sizeof p);
   p.case_id = CFD_RAYLEIGH_BENARD;
   p.check_every = 1;
-  p.ordering = CFD_ORDER_RB;
+  p.ordering = CFD_ORDER_RB;  // (no reference solver to reproduce; BASELINE configs[4] runs on ranks)
   p.nx = nx > 0 ? nx : 256;
   p.ny = ny > 0 ? ny : 64;
   p.ra = ra > 0 ? ra : 1e6;
@@ -146,4 +148,33 @@ extern "C" int cfd_params_init_rb(double ra, double pr, int nx, int ny, double d
   p.inlet_jmax = p.ny;
   *out = p;
   return CFD_OK;
+}
+
+// Launch-plan defaults that do not depend on the device (include/cfd_amd.h
+// cfd_tuning_default); Solver::init starts from these. Measured on MI355X
+// (DESIGN.md §4): cavity boundary-column bands 80 % of the interior march (open
+// cases 45 %); the channel's proof march fastest at a 16-row band floor, the
+// step's (and the cavity's) at 24; LDS tiles for the cavity only.
+extern "C" int cfd_tuning_default(const cfd_params* p, int knob, int* value) {
+  if (!p || !value) {
+    cfd::set_last_error("null argument");
+    return CFD_E_ARG;
+  }
+  const bool cav = p->case_id == CFD_CAVITY || p->case_id == CFD_RAYLEIGH_BENARD;
+  switch (knob) {
+    case CFD_TUNE_LEXW_EDGE_PCT: *value = 100; return CFD_OK;
+    case CFD_TUNE_PAIR_EDGE_PCT: *value = cav ? 80 : 45; return CFD_OK;
+    case CFD_TUNE_MARCH_MIN_TH: *value = p->case_id == CFD_CHANNEL ? 16 : 24; return CFD_OK;
+    case CFD_TUNE_TENT_TH: *value = 64; return CFD_OK;
+    case CFD_TUNE_LEXW_RAMP_PCT: *value = 0; return CFD_OK;
+    case CFD_TUNE_TILE_ROUNDS: *value = cav ? 1 : 0; return CFD_OK;
+    case CFD_TUNE_PAIR_WPS:
+    case CFD_TUNE_WAVE_WPS:
+    case CFD_TUNE_LEXW_WAVES:
+      cfd::set_last_error("this knob's default is derived from the device's occupancy at cfd_create");
+      return CFD_E_STATE;
+    default:
+      cfd::set_last_error("unknown tuning knob");
+      return CFD_E_ARG;
+  }
 }

@@ -21,6 +21,7 @@
 #include "small.hpp"
 #include "tile.hpp"
 #include "open.hpp"
+#include "smlex.hpp"
 
 namespace cfd {
 
@@ -200,6 +201,10 @@ class Solver {
 
   // cfd_set_tuning (include/cfd_amd.h enum cfd_tuning): launch planning only
   void set_tuning(int knob, int v) {
+    set_tuning_value(knob, v);
+    if (knob == CFD_TUNE_TILE_ROUNDS) plan_tiles();
+  }
+  void set_tuning_value(int knob, int v) {
     switch (knob) {
       case CFD_TUNE_PAIR_WPS: resident_pair_waves = std::max(1, std::min(v, 4)) * 4 * n_cu; break;
       case CFD_TUNE_WAVE_WPS: resident_waves = std::max(1, std::min(v, 4)) * 4 * n_cu; break;
@@ -209,10 +214,7 @@ class Solver {
       case CFD_TUNE_MARCH_MIN_TH: march_min_th = std::max(1, v); break;
       case CFD_TUNE_TENT_TH: tent_th = std::max(4, v); break;
       case CFD_TUNE_LEXW_RAMP_PCT: lexw_ramp_pct = std::max(0, std::min(100, v)); break;
-      case CFD_TUNE_TILE_ROUNDS:
-        tile_rounds = std::max(0, std::min(v, 16));
-        plan_tiles();
-        break;
+      case CFD_TUNE_TILE_ROUNDS: tile_rounds = std::max(0, std::min(v, 16)); break;
       default: throw Error(CFD_E_ARG, "unknown tuning knob");
     }
   }
@@ -293,17 +295,18 @@ class Solver {
       else
         HIPC(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pps, poisson_multi_kernel<BACKSTEP, 2>, 256, 0));
       pps = std::max(1, std::min(pps, 4));
-      if (P.case_id == CFD_CAVITY) {
-        // cavity launches (boundary-column waves with lane-constant indicators,
-        // nearly as fast as interior ones): boundary bands 80 % of the interior
-        // march; proof-mode launches planned for 2 waves per SIMD (taller
-        // bands: fewer halo rows), exact ones for 3 (measured at 4096^2,
-        // DESIGN.md §4)
-        pair_edge_pct = 80;
-        if (proof_ok()) pps = std::min(pps, 2);
-      } else {
-        tile_rounds = 0;
+      // device-independent plan defaults (params.cpp cfd_tuning_default):
+      // cavity boundary-column bands 80 % of the interior march (lane-constant
+      // indicators), the open cases 45 %; band floor 16 rows for the channel,
+      // 24 otherwise; LDS tiles for the cavity only
+      for (int knob : {CFD_TUNE_LEXW_EDGE_PCT, CFD_TUNE_PAIR_EDGE_PCT, CFD_TUNE_MARCH_MIN_TH, CFD_TUNE_TENT_TH,
+                       CFD_TUNE_LEXW_RAMP_PCT, CFD_TUNE_TILE_ROUNDS}) {
+        int v = 0;
+        if (cfd_tuning_default(&P, knob, &v) == CFD_OK) set_tuning_value(knob, v);
       }
+      // cavity proof-mode launches planned for 2 waves per SIMD (taller
+      // bands: fewer halo rows), exact ones for 3 (measured at 4096^2, §4)
+      if (P.case_id == CFD_CAVITY && proof_ok()) pps = std::min(pps, 2);
       if (use_lexw()) {
         int lps = 0;
         if (P.case_id == CFD_CHANNEL)
@@ -451,6 +454,8 @@ class Solver {
     ring = srcmax = divmax = tolv = total = partials = resmax = cscr = nullptr;
     if (lexbits) (void)hipFree(lexbits);
     lexbits = nullptr;
+    if (smlex_ck) (void)hipFree(smlex_ck);
+    smlex_ck = nullptr;
     lexbits_words = 0;
     if (stop) (void)hipFree(stop);
     stop = nullptr;
@@ -1372,7 +1377,50 @@ class Solver {
     return res;
   }
 
+  // the reference order on a reference-sized grid in one workgroup (smlex.hip):
+  // one strip, no ranks, p fits the LDS twice (small_solve = CFD_OFF: never)
+  double* smlex_ck = nullptr;  // its checkpoints (SMLEX_NCK fields of (nx+2)(ny+2) doubles)
+  bool use_smlex() const {
+    return P.ordering == CFD_ORDER_LEX && P.small_solve != CFD_OFF && S.size() == 1 && !comm && smlex_fits(S[0].g, C);
+  }
+
+  void solve_smlex(cfd_step_info* out) {
+    Strip& s = S[0];
+    double* X = s.b[pbuf(pcur)];
+    if (P.case_id == CFD_CAVITY)  // cavity-01.cpp:610-611: each solve starts from a zero field
+      HIPC(hipMemsetAsync(X, 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
+    if (!smlex_ck)
+      HIPC(hipMalloc(&smlex_ck, (size_t)SMLEX_NCK * (P.nx + 2) * (P.ny + 2) * sizeof(double)));
+    solve_tolerance();
+    int* d_it = stop;
+    double* d_res = total + 2;
+    HIPC(hipEventRecord(ev_a, st));
+    smlex_launch(P.case_id, s.g, C, X, s.b[B_F], tolv, P.max_iters, smlex_ck, d_it, d_res, st);
+    check_launch("poisson_smlex");
+    HIPC(hipEventRecord(ev_b, st));
+    int iters = 0;
+    double res = 0;
+    HIPC(hipMemcpyAsync(&iters, d_it, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPC(hipMemcpyAsync(&res, d_res, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
+    T.poisson_ms += ms;
+    T.poisson_launches += 1;
+    T.poisson_sweeps += iters;
+    T.poisson_cell_updates += (long long)P.nx * P.ny * iters;
+    if (out) {
+      out->sor_iterations = iters;
+      out->residual = res;
+    }
+  }
+
   void solve(cfd_step_info* out) {
+    if (use_smlex()) {
+      T.sor_kernel = CFD_SOR_SMLEX;
+      solve_smlex(out);
+      return;
+    }
     if (use_lexw()) {
       T.sor_kernel = CFD_SOR_LEXW;
       solve_lexw(out);
@@ -1789,6 +1837,10 @@ cfd_solver* cfd_create_rank(const cfd_params* p, int device, int row_begin, int 
   cfd_solver* out = nullptr;
   guard([&] {
     if (!p) throw Error(CFD_E_ARG, "null params");
+    // (cfd_params_init selects the reference order, which runs on one device: DESIGN.md §5)
+    if (p->ordering == CFD_ORDER_LEX)
+      throw Error(CFD_E_ARG, "lexicographic ordering runs on one device (strips allowed), not on ranks: "
+                             "cfd_create_rank needs ordering = CFD_ORDER_RB");
     if (row_begin < 1 || row_end > p->ny || row_end - row_begin + 1 < cfd::HALO)
       throw Error(CFD_E_ARG, "rank rows must lie in [1, ny] and span at least 8 rows (the SOR halo depth)");
     // the halo exchange talks to ranks rank-1 (rows below) and rank+1 (rows

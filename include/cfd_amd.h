@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 8
+#define CFD_AMD_ABI_VERSION 9
 
 /* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
  * tree (only figures): it is the cavity's projection step with a resting lid
@@ -68,16 +68,17 @@ typedef struct cfd_params {
   int step_i, inlet_jmax;  /* derived step indices (backwards_step-01.cpp:386, 493) */
   int check_every;      /* residual test every N SOR iterations (1 = reference) */
   int chunk;            /* SOR launches enqueued between host polls (0 = auto) */
-  int ordering;         /* CFD_ORDER_RB (red-black, strips/ranks) or CFD_ORDER_LEX (the reference's
-                           sweep order, bit-identical: every case at any size on one device, strips
-                           on that device allowed; a backwards step whose solid block is under 2
-                           cells wide or high runs on one workgroup, nx+ny < 12000) */
+  int ordering;         /* CFD_ORDER_LEX (cfd_params_init's default on one device: the reference's own
+                           sweep order, bit-identical to the reference binaries - every case at any size,
+                           strips on one device allowed) or CFD_ORDER_RB (red-black: the rank path, and
+                           faster where the reference's solve converges; required by cfd_create_rank) */
   int sweeps_per_launch; /* SOR iterations fused into one kernel launch, bit-identical for every value:
-                           0 = auto (red-black cavity: 4 in proof-mode launches, 3 in exact-residual
-                           ones; red-black channel / step: 2; lexicographic order: 4, 3 on strips);
-                           1, 2; 3 (cavity: every launch 3); 4 (red-black cavity with the proof test,
-                           or the lexicographic order: the auto plan, stated); 5 (lexicographic
-                           cavity on one strip) */
+                           0 = auto: red-black with the proof-mode test 4 (the backwards step on strips or
+                           ranks: 3), red-black with exact residuals 3 (cavity) / 2 (channel, step);
+                           lexicographic order 4 (3 on strips); 1, 2; 3 (red-black: cavity only, every
+                           launch 3); 4 (red-black with the proof test, or the lexicographic order: the
+                           auto plan, stated); 5 (lexicographic cavity on one strip). Ignored by the
+                           one-workgroup solves (small_solve) */
   /* Rayleigh-Benard (case 3), free-fall units: H = 1, U = sqrt(g beta dT H),
    * nu = sqrt(Pr/Ra), kappa = 1/sqrt(Ra Pr); hot bottom wall t_hot, cold top
    * wall t_cold, adiabatic side walls; buoyancy (T - t_ref) on v. */
@@ -85,10 +86,11 @@ typedef struct cfd_params {
   double t_perturb;     /* initial T = conduction profile + t_perturb*sin(pi y)cos(pi x/L) */
   /* Solve-path switches (enum cfd_switch; cfd_params_init sets CFD_AUTO). None of them changes a
    * result bit (iteration counts, residuals, fields); they choose how the same solve runs. */
-  int proof_test;       /* red-black cavity: proof-mode convergence test where it applies
-                           (AUTO / ON); OFF: the max-norm residual in every tested sweep */
-  int small_solve;      /* red-black, one strip, no ranks, p fits the LDS: the whole solve in one
-                           workgroup (small.hpp) (AUTO / ON); OFF: the multi-launch solve */
+  int proof_test;       /* red-black launches: proof-mode convergence test where it applies -
+                           every case (AUTO / ON); OFF: the max-norm residual in every tested sweep */
+  int small_solve;      /* one strip, no ranks, p fits the LDS: the whole solve in one workgroup - red-black
+                           (small.hpp) or the reference's order (smlex.hip) (AUTO / ON); OFF: the
+                           multi-launch solve */
   int overlap;          /* ranks with >= 48 rows: halo exchange overlapped with the interior rows
                            (AUTO / ON); OFF: exchange in front of each launch */
 } cfd_params;
@@ -132,7 +134,10 @@ enum cfd_sor_kernel {
   CFD_SOR_TILE = 2,   /* red-black LDS-tile launches (tile.hpp): one strip of up to ~4 M cells */
   CFD_SOR_SMALL = 3,  /* red-black whole solve in one workgroup (small.hpp): reference-sized grids */
   CFD_SOR_LEXW = 4,   /* reference order, multi-block march (lexw.hpp) */
-  CFD_SOR_LEX = 5     /* reference order, one workgroup (poisson_lex_kernel) */
+  CFD_SOR_LEX = 5,    /* reference order, one workgroup, global memory (poisson_lex_kernel: step geometries
+                         the other reference-order kernels do not take) */
+  CFD_SOR_SMLEX = 6   /* reference order, whole solve in one workgroup, p in LDS (smlex.hip): reference-sized
+                         grids (ABI 9) */
 };
 
 /* Library / ABI info. */
@@ -208,7 +213,8 @@ enum cfd_tuning {
   CFD_TUNE_LEXW_WAVES = 2,    /* tiles per lexicographic-order launch (>= 64) */
   CFD_TUNE_LEXW_EDGE_PCT = 3, /* wall-tile band length, % of the interior band (10..100) */
   CFD_TUNE_PAIR_EDGE_PCT = 4, /* boundary-column band length of red-black launches, % (10..100) */
-  CFD_TUNE_MARCH_MIN_TH = 5,  /* minimum rows per band of a march launch (>= 1) */
+  CFD_TUNE_MARCH_MIN_TH = 5,  /* minimum rows per band of a march launch (>= 1; default 16 for the channel,
+                                 24 otherwise) */
   CFD_TUNE_TENT_TH = 6,       /* rows per band of the predictor's march (>= 4) */
   CFD_TUNE_LEXW_RAMP_PCT = 7, /* lexicographic ramp launches: band height floor, % of the steady plan's (0..100) */
   CFD_TUNE_TILE_ROUNDS = 8    /* red-black, one strip: LDS-tile launches when the grid fits this many
@@ -216,6 +222,10 @@ enum cfd_tuning {
                                  default 1 for the cavity, 0 for the open cases) */
 };
 int cfd_set_tuning(cfd_solver* s, int knob, int value);
+/* The default a solver created from these parameters starts with (host only, no
+ * device needed; ABI 9). The waves-per-SIMD knobs (PAIR_WPS, WAVE_WPS,
+ * LEXW_WAVES) come from the device's occupancy: CFD_E_STATE. */
+int cfd_tuning_default(const cfd_params* p, int knob, int* value);
 
 /* Timing collected with HIP events on the solver's stream. */
 int cfd_get_timing(cfd_solver* s, cfd_timing* out);

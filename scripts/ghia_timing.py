@@ -14,7 +14,7 @@ import cfd_amd as C  # noqa: E402
 for small in ("on", "off"):
     for n, dt in ((63, 0.0), (96, 0.0), (128, 1e-3)):
         cp = C.make_params("cavity", re=100.0, nx=n, ny=n, dt=dt if dt > 0 else None)
-        s = C.solver_for(cp, small_solve=small)
+        s = C.solver_for(cp, ordering="rb", small_solve=small)
         s.applyBoundaryConditions()
         s.step()
         t0 = time.perf_counter()

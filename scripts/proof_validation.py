@@ -19,7 +19,7 @@ RUNS = [(256, 256, 300, 0), (500, 300, 100, 0), (1024, 1024, 6, 2000)]  # nx, ny
 
 def run(nx, ny, steps, cap, proof):
     cp = C.make_params("cavity", nx=nx, ny=ny, max_iters=cap or None)
-    s = C.solver_for(cp, small_solve="off", proof_test=proof)
+    s = C.solver_for(cp, ordering="rb", small_solve="off", proof_test=proof)
     s.applyBoundaryConditions()
     t0 = time.perf_counter()
     hist = [list(s.step()) for _ in range(steps)]

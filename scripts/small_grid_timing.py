@@ -1,57 +1,92 @@
 #!/usr/bin/env python3
-"""Reference-sized runs on the GPU (one-workgroup LDS solve, small.hpp) vs the
-reference's loop restated in C (oracle, lexicographic order, one core): the
-reference's default cavity run (63², cavity-01.cpp:311-318, run() loop) and
-the channel / step defaults, N steps each. Writes JSON to stdout."""
+"""Reference-sized runs (63², 93×31, 256×32: the reference binaries' own
+compiled-in cases) on the GPU in both sweep orders, next to the reference
+binary itself on the same host.
+
+  lex  — the reference's order, bit-identical to the reference binary
+         (the one-device default; its kernel family is reported);
+  rb   — red-black order (one-workgroup solve, small.hpp);
+  ref  — oracle/_ref/<case> (the unmodified reference, g++ -O2, one core),
+         timed from launch until it writes frame N (steps 1..N).
+
+Writes JSON to stdout (one object per case)."""
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "computational-fluid-dynamics_amd"))
-sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import torch  # noqa: E402,F401  (HIP runtime first)
 
 import cfd_amd as C  # noqa: E402
-import oracle as O  # noqa: E402
+from cfd_amd import _lib  # noqa: E402
+
+FRAME = {"cavity": ("cavity_flow", 100), "channel": ("channel_flow", 100), "backwards_step": ("backwards_step", 10)}
 
 
-def run(case, steps, cpu_steps):
+def gpu(case, ordering, steps):
     cp = C.reference_defaults(case)
-    g = C.solver_for(cp)
+    g = C.solver_for(cp, ordering=ordering)
     if case == "cavity":
         g.applyBoundaryConditions()
     g.step()
     g.synchronize()
+    g.reset_timing()
     t0 = time.perf_counter()
     its = [g.step()[0] for _ in range(steps)]
     g.synchronize()
-    gpu_s = time.perf_counter() - t0
+    el = time.perf_counter() - t0
     tm = g.timing()
     g.close()
-    o = O.Oracle(cp, ordering=O.LEX)
-    if case != "cavity":
-        o.velocity_bc(False)
-    o.step()
-    t0 = time.perf_counter()
-    cits = [o.step()[0] for _ in range(cpu_steps)]
-    cpu_s = time.perf_counter() - t0
-    cpu_per_step = cpu_s / cpu_steps
-    return {"case": case, "grid": f"{cp.nx}x{cp.ny}", "steps": steps,
-            "gpu_s": round(gpu_s, 4), "gpu_ms_per_step": round(gpu_s / steps * 1e3, 4),
-            "gpu_sor_iters_per_step": round(sum(its) / steps, 1),
-            "gpu_solve_launches": tm.poisson_launches,
-            "cpu_steps": cpu_steps, "cpu_ms_per_step": round(cpu_per_step * 1e3, 4),
-            "cpu_sor_iters_per_step": round(sum(cits) / cpu_steps, 1),
-            "cpu_kind": "oracle lexicographic loop (the reference's order), gcc -O2, 1 core",
-            "speedup_per_step": round(cpu_per_step / (gpu_s / steps), 2)}
+    return {"ms_per_step": round(el / steps * 1e3, 4), "steps": steps,
+            "sor_iters_per_step": round(sum(its) / steps, 1),
+            "launches_per_step": round(tm.poisson_launches / steps, 1),
+            "sor_kernel": _lib.SOR_KERNEL.get(tm.sor_kernel, "?"),
+            "us_per_iteration": round(el / max(sum(its), 1) * 1e6, 3)}
+
+
+def reference_binary(case, timeout_s=120.0):
+    exe = os.path.join(ROOT, "oracle", "_ref", case)
+    if not os.path.exists(exe):
+        return None
+    base, n = FRAME[case]
+    wd = tempfile.mkdtemp(prefix="cfd_ref_")
+    try:
+        t0 = time.perf_counter()
+        proc = subprocess.Popen([exe], cwd=wd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        frame = os.path.join(wd, "vtk_output", f"{base}_{n:06d}.vtk")
+        while not os.path.exists(frame) and proc.poll() is None and time.perf_counter() - t0 < timeout_s:
+            time.sleep(0.01)
+        el = time.perf_counter() - t0
+        ok = os.path.exists(frame)
+        proc.kill()
+        proc.wait()
+    finally:
+        shutil.rmtree(wd, ignore_errors=True)
+    return {"ms_per_step": round(el / n * 1e3, 3), "steps": n, "cores": 1,
+            "kind": "reference binary (unmodified source, g++ -O2), steps 1..N incl. frame output"} if ok else None
 
 
 if __name__ == "__main__":
+    plan = [("cavity", 500), ("channel", 100), ("backwards_step", 20)]
+    if len(sys.argv) > 1:
+        plan = [p for p in plan if p[0] in sys.argv[1:]]
     out = []
-    for case, n, ncpu in (("cavity", 2519, 300), ("channel", 100, 20), ("backwards_step", 50, 10)):
-        out.append(run(case, n, ncpu))
-        print(json.dumps(out[-1]), file=sys.stderr, flush=True)
+    for case, n in plan:
+        r = {"case": case, "grid": "{}x{}".format(*(lambda c: (c.nx, c.ny))(C.reference_defaults(case)))}
+        r["lex"] = gpu(case, "lex", n)
+        print(json.dumps(r), file=sys.stderr, flush=True)
+        r["rb"] = gpu(case, "rb", n)
+        print(json.dumps(r), file=sys.stderr, flush=True)
+        r["ref"] = reference_binary(case)
+        if r["ref"]:
+            r["lex_speedup_vs_ref"] = round(r["ref"]["ms_per_step"] / r["lex"]["ms_per_step"], 2)
+            r["rb_speedup_vs_ref"] = round(r["ref"]["ms_per_step"] / r["rb"]["ms_per_step"], 2)
+        out.append(r)
+        print(json.dumps(r), file=sys.stderr, flush=True)
     print(json.dumps(out, indent=1))

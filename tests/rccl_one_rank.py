@@ -28,7 +28,7 @@ def main() -> int:
     comm = init_comm(dist, 0, 1, 0)
     info = comm_info(comm)
     cp = C.reference_defaults(case)
-    s = C.solver_for(cp, rank_rows=strip_rows(0, 1, cp.ny), comm=comm, check_every=1)
+    s = C.solver_for(cp, ordering="rb", rank_rows=strip_rows(0, 1, cp.ny), comm=comm, check_every=1)
     if case == "cavity":
         s.applyBoundaryConditions()
     its = [s.step() for _ in range(steps)]
@@ -36,7 +36,7 @@ def main() -> int:
     s.close()
     _lib.lib().cfd_comm_destroy(comm)
 
-    r = C.solver_for(cp)
+    r = C.solver_for(cp, ordering="rb")
     if case == "cavity":
         r.applyBoundaryConditions()
     its_ref = [r.step() for _ in range(steps)]

@@ -27,7 +27,7 @@ def rank_main(rank, world, case, ny, steps, q):
     comm = init_comm(dist, rank, world, rank)
     info = comm_info(comm)
     cp = C.make_params(case, nx=96, ny=ny)
-    s = C.solver_for(cp, device=rank, rank_rows=strip_rows(rank, world, ny), comm=comm, check_every=1)
+    s = C.solver_for(cp, ordering="rb", device=rank, rank_rows=strip_rows(rank, world, ny), comm=comm, check_every=1)
     if case == "cavity":
         s.applyBoundaryConditions()
     its = [s.step() for _ in range(steps)]
@@ -37,7 +37,7 @@ def rank_main(rank, world, case, ny, steps, q):
     s.close()
     dist.barrier()
     _lib.lib().cfd_comm_destroy(comm)
-    r = C.solver_for(cp, device=rank)
+    r = C.solver_for(cp, ordering="rb", device=rank)
     if case == "cavity":
         r.applyBoundaryConditions()
     its_ref = [r.step() for _ in range(steps)]

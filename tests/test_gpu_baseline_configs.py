@@ -33,7 +33,7 @@ from test_gpu_ranks import run_ranks  # noqa: E402
 def test_config0_cavity_re100_128_bitexact_and_reference_order():
     cp = C.make_params("cavity", re=100.0, nx=128, ny=128, dt=1e-3)
     assert cp.total_steps == 20000 and cp.nu == pytest.approx(0.01)
-    g = C.CavitySolver(cp)
+    g = C.CavitySolver(cp, ordering="rb")
     orb = O.Oracle(cp, ordering=O.RB)
     olex = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
@@ -57,7 +57,7 @@ def test_config0_cavity_re100_128_bitexact_and_reference_order():
 
 def test_config1_cavity_1024_steps_bitexact_capped():
     cp = C.make_params("cavity", re=1000.0, nx=1024, ny=1024, max_iters=300)
-    g = C.CavitySolver(cp)
+    g = C.CavitySolver(cp, ordering="rb")
     o = O.Oracle(cp, ordering=O.RB)
     g.applyBoundaryConditions()
     for k in range(2):
@@ -77,7 +77,7 @@ def test_config1_cavity_1024_full_step_meets_reference_stop_rule():
     converging solve is checked bit-exactly against the oracle at reference
     sizes, tests/test_gpu_parity.py.)"""
     cp = C.make_params("cavity", re=1000.0, nx=1024, ny=1024)
-    g = C.CavitySolver(cp)
+    g = C.CavitySolver(cp, ordering="rb")
     g.applyBoundaryConditions()
     g.computeTentativeVelocities()
     g.buildSourceTerm()
@@ -109,7 +109,7 @@ def test_config3_backstep_8192x512_four_ranks_vs_oracle():
 
 def test_config4_rayleigh_benard_8192x2048_step_vs_oracle():
     cp = C.make_params("rayleigh_benard", ra=1e6, pr=0.71, nx=8192, ny=2048, max_iters=30)
-    g = C.RayleighBenardSolver(cp)
+    g = C.RayleighBenardSolver(cp, ordering="rb")
     o = O.Oracle(cp, ordering=O.RB)
     assert g.step() == o.step()
     for name in ("u", "v", "p"):
@@ -119,8 +119,8 @@ def test_config4_rayleigh_benard_8192x2048_step_vs_oracle():
 
 def test_config4_rayleigh_benard_8192x2048_strips_equal_single_domain():
     cp = C.make_params("rayleigh_benard", ra=1e6, pr=0.71, nx=8192, ny=2048, max_iters=60)
-    a = C.RayleighBenardSolver(cp)
-    b = C.RayleighBenardSolver(cp, n_strips=4)
+    a = C.RayleighBenardSolver(cp, ordering="rb")
+    b = C.RayleighBenardSolver(cp, ordering="rb", n_strips=4)
     for _ in range(2):
         assert a.step() == b.step()
     for name in ("u", "v", "p", "t"):

@@ -25,6 +25,59 @@ def run(name, *args, cwd):
     return ANSI.sub("", r.stdout).splitlines(), ANSI.sub("", r.stderr).splitlines()
 
 
+BASE = {"cavity": "cavity_flow", "channel": "channel_flow", "backwards_step": "backwards_step"}
+
+
+@pytest.mark.parametrize("name", ["cavity", "channel"])
+def test_default_binary_is_the_reference(name, tmp_path):
+    """With no flags, each drop-in binary runs the reference's whole default
+    case (cavity 63^2 2520 steps, channel 93x31 1537 steps) and prints the
+    reference binary's log line for line - every Step line and every
+    capped-solve warning - and writes its frame files byte for byte."""
+    out, err = run(name, cwd=tmp_path)
+    assert [l for l in out if l.startswith("Step ")] == LOGS[name]["steps"]
+    assert [l for l in err if "Warning" in l] == LOGS[name]["warnings"]
+    for h in LOGS[name]["header"]:
+        assert h in out, h
+    vtk = tmp_path / "vtk_output"
+    assert (vtk / f"{BASE[name]}_animation.pvd").exists()
+    for fr, digest in LOGS[name]["vtk_sha256"].items():
+        data = (vtk / f"{BASE[name]}_{int(fr):06d}.vtk").read_bytes()
+        assert hashlib.sha256(data).hexdigest() == digest, fr
+
+
+def test_default_step_binary_is_the_reference(tmp_path):
+    """bin/backwards_step with no flags: its first 20 steps (the reference's
+    case caps at 10000 sweeps on nearly every step; the fixtures hold steps
+    1-20, tests/golden/make_golden.py) print the reference's Step lines and
+    capped-solve warnings and write its frames 0, 10 and 20 byte for byte;
+    the run is then stopped."""
+    import time
+    proc = subprocess.Popen([os.path.join(BIN, "backwards_step")], cwd=tmp_path, stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True)
+    steps, t0 = [], time.time()
+    try:
+        for line in proc.stdout:
+            line = ANSI.sub("", line.rstrip("\n"))
+            if line.startswith("Step "):
+                steps.append(line)
+                if len(steps) == len(LOGS["backwards_step"]["steps"]):
+                    break
+            assert time.time() - t0 < 120
+        nxt = tmp_path / "vtk_output" / "backwards_step_000030.vtk"  # (frame 20 is closed once 30 exists)
+        while not nxt.exists() and time.time() - t0 < 120:
+            time.sleep(0.05)
+    finally:
+        proc.kill()
+        _, err = proc.communicate()
+    assert steps == LOGS["backwards_step"]["steps"]
+    warns = [ANSI.sub("", l) for l in err.splitlines() if "Warning" in l]
+    assert len(warns) >= 20 and warns == LOGS["backwards_step"]["warnings"][: len(warns)]
+    for fr, digest in LOGS["backwards_step"]["vtk_sha256"].items():
+        data = (tmp_path / "vtk_output" / f"backwards_step_{int(fr):06d}.vtk").read_bytes()
+        assert hashlib.sha256(data).hexdigest() == digest, fr
+
+
 @pytest.mark.parametrize("name,steps", [("cavity", 200), ("channel", 200), ("backwards_step", 20)])
 def test_exact_binary_prints_reference_log(name, steps, tmp_path):
     out, err = run(name, "--exact", "--steps", str(steps), "--no-vtk", cwd=tmp_path)
@@ -87,7 +140,7 @@ def test_rayleigh_benard_python_run_matches_binary(tmp_path):
                  "--output-dir", "bin_out", cwd=tmp_path)
     cp = C.make_params("rayleigh_benard", nx=64, ny=16, ra=5e4, max_iters=2000)
     cp.print_interval = cp.save_interval = 20
-    s = C.RayleighBenardSolver(cp)
+    s = C.RayleighBenardSolver(cp, ordering="rb")
     buf = io.StringIO()
     s.run(output_directory=str(tmp_path / "py_out"), out=buf, err=io.StringIO(), steps=40)
     py_steps = [l for l in buf.getvalue().splitlines() if l.startswith("Step ")]

@@ -24,7 +24,7 @@ from test_gpu_ranks import run_ranks, single  # noqa: E402
 def test_channel_poiseuille_profile():
     # viscous development time H^2 / nu = 10: run to t = 25
     cp = C.make_params("channel", re=10.0, nx=96, ny=32, final_time=25.0)
-    s = C.ChannelSolver(cp)
+    s = C.ChannelSolver(cp, ordering="rb")
     s.run_steps(cp.total_steps)
     s.statistics()
     uc = s.field("uc")
@@ -51,7 +51,7 @@ def test_channel_poiseuille_profile():
 
 def test_channel_re1000_4096x512_runs():
     cp = C.make_params("channel", re=1000.0, nx=4096, ny=512, max_iters=2000)
-    s = C.ChannelSolver(cp)
+    s = C.ChannelSolver(cp, ordering="rb")
     for _ in range(3):
         it, res = s.step()
         assert 1 <= it <= cp.max_iters and np.isfinite(res)

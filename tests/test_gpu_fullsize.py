@@ -61,7 +61,7 @@ def cavity_residual(p, f, dx):
 
 def test_cavity_4096_step_bitexact_vs_red_black_oracle():
     cp = cavity(max_iters=30)
-    g = C.solver_for(cp)
+    g = C.solver_for(cp, ordering="rb")
     o = O.Oracle(cp, ordering=O.RB)
     ig, rg = g.step()
     io, ro = o.step()
@@ -73,7 +73,7 @@ def test_cavity_4096_step_bitexact_vs_red_black_oracle():
 
 def test_channel_4096x512_step_vs_red_black_oracle():
     cp = C.make_params("channel", re=1000.0, nx=4096, ny=512, max_iters=30)
-    g = C.solver_for(cp)
+    g = C.solver_for(cp, ordering="rb")
     o = O.Oracle(cp, ordering=O.RB)
     o.velocity_bc(False)
     ig, _ = g.step()
@@ -87,7 +87,7 @@ def test_channel_4096x512_step_vs_red_black_oracle():
 
 def test_cavity_4096_reported_residual_is_true_residual():
     cp = cavity(max_iters=200)
-    g = C.solver_for(cp)
+    g = C.solver_for(cp, ordering="rb")
     predictor_source(g)
     it, res = g.solverPressurePoisson()
     assert it == 200
@@ -97,7 +97,7 @@ def test_cavity_4096_reported_residual_is_true_residual():
 
 def test_cavity_4096_poisson_homogeneous_in_source():
     cp = cavity(max_iters=10000)
-    g = C.solver_for(cp)
+    g = C.solver_for(cp, ordering="rb")
     rng = np.random.default_rng(11)
     f = np.zeros((N + 2, N + 2))
     # smooth source so the solve converges in a few hundred sweeps at 4096²
@@ -117,8 +117,8 @@ def test_cavity_4096_poisson_homogeneous_in_source():
 
 def test_cavity_4096_strips_equal_single_domain():
     cp = cavity(max_iters=50)
-    a = C.solver_for(cp, n_strips=1)
-    b = C.solver_for(cp, n_strips=4)
+    a = C.solver_for(cp, ordering="rb", n_strips=1)
+    b = C.solver_for(cp, ordering="rb", n_strips=4)
     for _ in range(2):
         ia, ra = a.step()
         ib, rb = b.step()

@@ -35,7 +35,7 @@ GHIA_V = np.array([
 
 def ghia_deviation(n, dt, t_end):
     cp = C.make_params("cavity", re=100.0, nx=n, ny=n, dt=dt)
-    s = C.solver_for(cp)
+    s = C.solver_for(cp, ordering="rb")
     s.applyBoundaryConditions()
     t0 = time.perf_counter()
     steps = int(round(t_end / dt))

@@ -27,7 +27,7 @@ MARCH = {"tile_rounds": 0}  # the wave march (the LDS tiles have their own tests
 
 
 def run(case, cp, steps, strips=1, **kw):
-    g = SOLVERS[case](cp, device=0, small_solve="off", n_strips=strips, tuning=MARCH, **kw)
+    g = SOLVERS[case](cp, ordering="rb", device=0, small_solve="off", n_strips=strips, tuning=MARCH, **kw)
     hist = [g.step() for _ in range(steps)]
     out = {n: g.field(n).copy() for n in FIELDS}
     tm = g.timing()
@@ -71,7 +71,7 @@ def test_open_proof_vs_red_black_oracle(case, nx, ny, cap):
     rng = np.random.default_rng(11)
     f = rng.standard_normal((cp.ny + 2, cp.nx + 2))
     p0 = rng.standard_normal((cp.ny + 2, cp.nx + 2))
-    g = SOLVERS[case](cp, device=0, small_solve="off", tuning=MARCH)
+    g = SOLVERS[case](cp, ordering="rb", device=0, small_solve="off", tuning=MARCH)
     o = O.Oracle(cp, ordering=O.RB)
     g.set_field("src", f)
     o.field("src")[...] = f

@@ -33,7 +33,7 @@ FIELDS = ("p", "u", "v")
 
 
 def run(case, cp, steps, **kw):
-    g = SOLVERS[case](cp, device=0, **MULTI, **kw)
+    g = SOLVERS[case](cp, ordering="rb", device=0, **MULTI, **kw)
     hist = [g.step() for _ in range(steps)]
     out = {n: g.field(n).copy() for n in FIELDS}
     tm = g.timing()
@@ -58,7 +58,7 @@ def test_pairs_equal_single_sweeps(case, spl):
 @pytest.mark.parametrize("spl", [2, 3])
 def test_stop_inside_a_launch_is_replayed_and_matches_oracle(spl):
     cp = C.reference_defaults("cavity")
-    g = C.CavitySolver(cp, device=0, sweeps_per_launch=spl, **MULTI)
+    g = C.CavitySolver(cp, ordering="rb", device=0, sweeps_per_launch=spl, **MULTI)
     o = O.Oracle(cp, ordering=O.RB)
     it_g, res_g = g.step()
     it_o, res_o = o.step()
@@ -80,7 +80,7 @@ def test_iteration_cap_edges(spl, delta):
     shorter last launches), at K, and above K (the stop found by a launch, or
     by the host's test of the iterations no launch tested)."""
     base = C.reference_defaults("cavity")
-    K, _ = C.CavitySolver(base, device=0, sweeps_per_launch=1, **MULTI).step()
+    K, _ = C.CavitySolver(base, ordering="rb", device=0, sweeps_per_launch=1, **MULTI).step()
     cp = C.make_params("cavity", max_iters=K + delta)
     h1, f1, _ = run("cavity", cp, 1, sweeps_per_launch=1)
     h2, f2, _ = run("cavity", cp, 1, sweeps_per_launch=spl)

@@ -78,7 +78,7 @@ def rel_l2(a, b):
 @pytest.mark.parametrize("case", CASES)
 def test_stencil_phases_bitexact(case, strips):
     cp = small_params(case)
-    g = C.solver_for(cp, n_strips=strips)
+    g = C.solver_for(cp, ordering="rb", n_strips=strips)
     o = O.Oracle(cp)
     rng = np.random.default_rng(1234)
     nx, ny = cp.nx, cp.ny
@@ -130,7 +130,7 @@ def test_stencil_phases_bitexact(case, strips):
 def test_poisson_rb_bitexact(case, strips):
     """The fused red-black kernel == the oracle's red-black restatement, bit for bit."""
     cp = small_params(case, max_iters=3000)
-    g = C.solver_for(cp, n_strips=strips)
+    g = C.solver_for(cp, ordering="rb", n_strips=strips)
     o = O.Oracle(cp, ordering=O.RB)
     rng = np.random.default_rng(7)
     nx, ny = cp.nx, cp.ny
@@ -154,7 +154,7 @@ def test_poisson_converges_to_reference_solution(case):
     """Red-black vs the reference's lexicographic SOR: same fixed point to tolerance
     (cases whose reference solve converges; see test_oracle_golden for the step)."""
     cp = small_params(case, max_iters=10000)
-    g = C.solver_for(cp)
+    g = C.solver_for(cp, ordering="rb")
     o = O.Oracle(cp, ordering=O.LEX)
     if case != "cavity":
         g.applyBoundaryConditions()
@@ -187,7 +187,7 @@ def test_run_matches_reference_algorithm(case, steps):
     centerline velocity scale (the channel's horizontal-centerline v is ~0 by
     symmetry, so normalising by ||v_ref|| would measure round-off)."""
     cp = small_params(case)
-    g = C.solver_for(cp)
+    g = C.solver_for(cp, ordering="rb")
     olex = O.Oracle(cp, ordering=O.LEX)
     orb = O.Oracle(cp, ordering=O.RB)
     if case != "cavity":
@@ -217,7 +217,7 @@ def test_backstep_run_matches_red_black_oracle():
     to its own CPU restatement (same ordering): equal up to the source-mean
     re-association (1e-10), iteration counts equal."""
     cp = small_params("backwards_step")
-    g = C.solver_for(cp)
+    g = C.solver_for(cp, ordering="rb")
     orb = O.Oracle(cp, ordering=O.RB)
     orb.velocity_bc(False)
     for _ in range(3):
@@ -233,8 +233,8 @@ def test_backstep_run_matches_red_black_oracle():
 def test_strips_equal_single_domain(case):
     cp = small_params(case)
     steps = 3 if case == "backwards_step" else 20
-    a = C.solver_for(cp, n_strips=1)
-    b = C.solver_for(cp, n_strips=min(4, cp.ny // 8))  # each strip owns >= HALO (8) rows
+    a = C.solver_for(cp, ordering="rb", n_strips=1)
+    b = C.solver_for(cp, ordering="rb", n_strips=min(4, cp.ny // 8))  # each strip owns >= HALO (8) rows
     for _ in range(steps):
         ia, _ = a.step()
         ib, _ = b.step()
@@ -251,7 +251,7 @@ def test_strips_equal_single_domain(case):
 def test_cavity_final_frame_matches_reference_output():
     """Full reference run (63^2, Re 1000, 2520 steps) against its own VTK output."""
     cp = C.reference_defaults("cavity")
-    g = C.CavitySolver(cp)
+    g = C.CavitySolver(cp, ordering="rb")
     g.applyBoundaryConditions()
     g.run_steps(cp.total_steps)
     g.statistics()
@@ -273,7 +273,7 @@ def test_log_lines_match_reference_format():
     """run() prints the reference's log lines; iteration counts differ only by ordering."""
     import io
     cp = C.reference_defaults("channel")
-    g = C.ChannelSolver(cp)
+    g = C.ChannelSolver(cp, ordering="rb")
     out, err = io.StringIO(), io.StringIO()
     g.run(output_directory=None, out=out, err=err, steps=200)
     lines = out.getvalue().splitlines()

@@ -30,7 +30,7 @@ def run(monkeypatch, cp, steps, proof, ns=3, last_timing=False, **kw):
     residual stage, so four sweeps fit the 8-row halos); else exact residuals.
     Always the multi-launch solve (small_solve off), at any size.
     last_timing: timing of the last step only."""
-    g = C.CavitySolver(cp, device=0, small_solve="off", tuning=MARCH, proof_test="on" if proof else "off",
+    g = C.CavitySolver(cp, ordering="rb", device=0, small_solve="off", tuning=MARCH, proof_test="on" if proof else "off",
                        sweeps_per_launch=ns if proof else 0, **kw)
     hist = []
     for s in range(steps):
@@ -123,7 +123,7 @@ def test_full_size_step_proven(monkeypatch, ns):
 
 def solve_source(cp, f, proof, chunk=0):
     """solverPressurePoisson on a given source (cavity: from a zero field)."""
-    g = C.CavitySolver(cp, device=0, small_solve="off", tuning=MARCH, proof_test="on" if proof else "off",
+    g = C.CavitySolver(cp, ordering="rb", device=0, small_solve="off", tuning=MARCH, proof_test="on" if proof else "off",
                        sweeps_per_launch=4 if proof else 0, chunk=chunk)
     g.set_field("src", f)
     it, res = g.solverPressurePoisson()
@@ -145,7 +145,7 @@ def test_stop_in_first_proof_launch_after_fallback():
     tolerance is placed at the exact residual of each iteration 12..26: every
     solve must equal exact residuals throughout, bit for bit."""
     base = C.make_params("cavity", nx=256, ny=256)
-    g = C.CavitySolver(base, device=0, small_solve="off", tuning=MARCH)
+    g = C.CavitySolver(base, ordering="rb", device=0, small_solve="off", tuning=MARCH)
     g.applyBoundaryConditions()
     g.computeTentativeVelocities()
     g.buildSourceTerm()

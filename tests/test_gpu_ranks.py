@@ -29,7 +29,7 @@ def run_ranks(cp, world, steps, check_every=1, timing=False, **kw):
         try:
             comm = L.cfd_comm_init_loopback(hub, r, 0)
             assert comm, L.cfd_last_error()
-            s = C.solver_for(cp, rank_rows=strip_rows(r, world, cp.ny), comm=comm, check_every=check_every, **kw)
+            s = C.solver_for(cp, ordering="rb", rank_rows=strip_rows(r, world, cp.ny), comm=comm, check_every=check_every, **kw)
             if cp.case_id == C.CAVITY:
                 s.applyBoundaryConditions()
             its = [s.step() for _ in range(steps)]
@@ -53,7 +53,7 @@ def run_ranks(cp, world, steps, check_every=1, timing=False, **kw):
 
 
 def single(cp, steps, **kw):
-    s = C.solver_for(cp, **kw)
+    s = C.solver_for(cp, ordering="rb", **kw)
     if cp.case_id == C.CAVITY:
         s.applyBoundaryConditions()
     its = [s.step() for _ in range(steps)]

@@ -31,7 +31,7 @@ def rb(**kw):
 
 def test_initial_temperature_matches_oracle():
     cp = rb()
-    g = C.RayleighBenardSolver(cp)
+    g = C.RayleighBenardSolver(cp, ordering="rb")
     o = O.Oracle(cp, ordering=O.RB)
     assert_bits(g.field("t"), o.field("t"), "T0")
 
@@ -39,7 +39,7 @@ def test_initial_temperature_matches_oracle():
 def test_stages_bit_exact():
     """One step stage by stage: velocity BCs, predictor, thermal, source, SOR, correction."""
     cp = rb()
-    g = C.RayleighBenardSolver(cp)
+    g = C.RayleighBenardSolver(cp, ordering="rb")
     o = O.Oracle(cp, ordering=O.RB)
     g.applyBoundaryConditions()
     o.velocity_bc()
@@ -66,7 +66,7 @@ def test_stages_bit_exact():
 @pytest.mark.parametrize("n_strips", [1, 3])
 def test_steps_bit_exact(n_strips):
     cp = rb(nx=64, ny=48)
-    g = C.RayleighBenardSolver(cp, n_strips=n_strips)
+    g = C.RayleighBenardSolver(cp, ordering="rb", n_strips=n_strips)
     o = O.Oracle(cp, ordering=O.RB)
     for k in range(12):
         gs = g.step()
@@ -85,7 +85,7 @@ def test_rank_path_equals_single_domain():
     """Loopback ranks (the RCCL code path) == one domain, bit for bit."""
     cp = rb(nx=64, ny=64)
     res = run_ranks(cp, 2, 8)
-    s = C.RayleighBenardSolver(cp)
+    s = C.RayleighBenardSolver(cp, ordering="rb")
     its = [s.step() for _ in range(8)]
     assert res[0]["its"] == its and res[1]["its"] == its
     p = s.field("p")
@@ -102,7 +102,7 @@ def test_onset_and_heat_transport():
     out = {}
     for ra in (1e3, 5e4):
         cp = rb(nx=64, ny=16, ra=ra, max_iters=2000)
-        g = C.RayleighBenardSolver(cp)
+        g = C.RayleighBenardSolver(cp, ordering="rb")
         ke = []
         for n in range(1200):
             g.step()

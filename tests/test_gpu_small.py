@@ -19,7 +19,7 @@ from test_gpu_parity import assert_bits, ofield  # noqa: E402
 
 
 def run_gpu(cp, steps, small=True, cavity=True, **kw):
-    g = C.solver_for(cp, small_solve="on" if small else "off", **kw)
+    g = C.solver_for(cp, ordering="rb", small_solve="on" if small else "off", **kw)
     if cavity:  # cavity-01.cpp:380 (the open cases apply their BCs in the constructor)
         g.applyBoundaryConditions()
     its = [g.step() for _ in range(steps)]

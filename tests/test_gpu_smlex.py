@@ -1,0 +1,120 @@
+"""The reference's order on reference-sized grids in one workgroup
+(smlex.hip): bit for bit the oracle's lexicographic loop (ORC_LEX, pinned to
+the reference binaries in test_oracle_golden.py) and the multi-block
+reference-order march (lexw.hpp), whatever the stop: converged (replay from a
+checkpoint or from the initial field) or capped (every iteration count around
+the checkpoint interval M)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import cfd_amd as C  # noqa: E402
+from cfd_amd import _lib  # noqa: E402
+import oracle as O  # noqa: E402
+
+
+def bits_equal(a, b):
+    return np.array_equal(np.asarray(a).view(np.int64), np.asarray(b).view(np.int64))
+
+
+def interval(cp):  # smlex.hip smlex_interval
+    m = 8
+    while m < (cp.nx + cp.ny) // 6 + 2:
+        m *= 2
+    return m
+
+
+def run_pair(cp, steps, small="auto"):
+    g = C.solver_for(cp, ordering="lex", small_solve=small)
+    o = O.Oracle(cp, ordering=O.LEX)
+    if cp.case_id == C.params.CAVITY:
+        g.applyBoundaryConditions()
+    o.velocity_bc(False)
+    its = []
+    for k in range(steps):
+        ig, rg = g.step()
+        io_, ro = o.step()
+        assert (ig, rg) == (io_, ro), (k, ig, io_, rg, ro)
+        its.append(ig)
+    nx, ny = cp.nx, cp.ny
+    assert bits_equal(g.field("p"), o.field("p"))
+    assert bits_equal(g.field("u"), o.field("u")[:, : nx + 1])
+    assert bits_equal(g.field("v"), o.field("v")[: ny + 1, :])
+    return g, its
+
+
+@pytest.mark.parametrize("case,steps", [("cavity", 40), ("channel", 25), ("backwards_step", 3)])
+def test_reference_defaults_run_smlex_bitexact(case, steps):
+    """The reference's own runs take the one-workgroup kernel by default and
+    match the oracle's reference loop bit for bit (converging solves: replay
+    from a checkpoint; the step: capped solves)."""
+    cp = C.reference_defaults(case)
+    g, its = run_pair(cp, steps)
+    assert _lib.SOR_KERNEL[g.timing().sor_kernel] == "smlex"
+    assert g.timing().poisson_launches == steps  # one launch per solve
+
+
+@pytest.mark.parametrize("case,nx,ny", [("cavity", 37, 21), ("cavity", 20, 45), ("channel", 50, 17),
+                                        ("channel", 31, 31), ("backwards_step", 60, 20), ("backwards_step", 41, 13)])
+def test_odd_grids_converging_bitexact(case, nx, ny):
+    cp = C.make_params(case, nx=nx, ny=ny)
+    run_pair(cp, 6)
+
+
+@pytest.mark.parametrize("case", ["cavity", "channel", "backwards_step"])
+def test_caps_around_checkpoints_bitexact(case):
+    """Capped solves of every length around the checkpoint interval: the
+    last iteration's refresh duties (ghosts / solids at the refresh after
+    iteration K-1, then the final refresh), K = 1 included."""
+    base = C.make_params(case, nx=40, ny=24)
+    M = interval(base)
+    for cap in (1, 2, 3, M - 1, M, M + 1, 2 * M + 1):
+        cp = C.make_params(case, nx=40, ny=24, max_iters=cap)
+        _, its = run_pair(cp, 3)
+        assert all(i <= cap for i in its)
+
+
+@pytest.mark.parametrize("case", ["cavity", "channel", "backwards_step"])
+def test_early_convergence_replays_from_initial_field(case):
+    """Loose tolerances stop solves before the first checkpoint (the replay
+    restarts from the solve's initial field), near it and past it; a solve
+    the loop never enters (0 iterations) leaves the field as the reference
+    does."""
+    its = []
+    for tf in (1e-1, 1e-2, 1e-3, 1e-4, 1e-5):
+        cp = C.make_params(case, nx=48, ny=30)
+        cp.tol_factor = tf
+        its += run_pair(cp, 4)[1]
+    M = interval(C.make_params(case, nx=48, ny=30))
+    assert any(1 <= i < M for i in its), its
+    assert any(i > M for i in its), its
+
+
+@pytest.mark.parametrize("case,steps", [("cavity", 12), ("channel", 8), ("backwards_step", 2)])
+def test_smlex_equals_multiblock_march(case, steps):
+    """One workgroup vs the multi-block reference-order march (lexw.hpp) on the
+    same run: the same iteration counts, residuals and fields, bit for bit."""
+    cp = C.reference_defaults(case)
+    a = C.solver_for(cp, ordering="lex")
+    b = C.solver_for(cp, ordering="lex", small_solve="off")
+    if case == "cavity":
+        a.applyBoundaryConditions()
+        b.applyBoundaryConditions()
+    for _ in range(steps):
+        assert a.step() == b.step()
+    assert _lib.SOR_KERNEL[a.timing().sor_kernel] == "smlex"
+    assert _lib.SOR_KERNEL[b.timing().sor_kernel] == "lexw"
+    for f in ("p", "u", "v"):
+        assert bits_equal(a.field(f), b.field(f)), f
+
+
+def test_large_grid_keeps_multiblock_march():
+    """Past the LDS (p and its previous values: (nx+2)(ny+2) <= 10048) the
+    reference order runs the multi-block march."""
+    g = C.solver_for(C.make_params("cavity", nx=128, ny=128), ordering="lex")
+    g.applyBoundaryConditions()
+    g.step()
+    assert _lib.SOR_KERNEL[g.timing().sor_kernel] == "lexw"

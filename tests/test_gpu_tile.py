@@ -33,7 +33,7 @@ TILES = {"tile_rounds": 1}
 
 def run(case, cp, steps, tile_rounds=None, **kw):
     tuning = {"tile_rounds": 1 if tile_rounds is None else tile_rounds}
-    g = SOLVERS[case](cp, device=0, small_solve="off", tuning=tuning, **kw)
+    g = SOLVERS[case](cp, ordering="rb", device=0, small_solve="off", tuning=tuning, **kw)
     if case == "cavity":
         g.applyBoundaryConditions()
     hist = [g.step() for _ in range(steps)]
@@ -82,7 +82,7 @@ def test_tile_vs_red_black_oracle(case, cap, tol):
     rng = np.random.default_rng(7)
     f = rng.standard_normal((cp.ny + 2, cp.nx + 2))
     p0 = rng.standard_normal((cp.ny + 2, cp.nx + 2)) * (0.0 if case == "cavity" else 1.0)
-    g = SOLVERS[case](cp, device=0, small_solve="off", tuning=TILES)
+    g = SOLVERS[case](cp, ordering="rb", device=0, small_solve="off", tuning=TILES)
     o = O.Oracle(cp, ordering=O.RB)
     g.set_field("src", f)
     o.field("src")[...] = f
@@ -117,7 +117,7 @@ def test_tile_stop_inside_launch_and_explicit_sweeps(spl):
     """Converging solves (the reference's 63^2 cavity on the tile path): stops
     inside a launch are replayed from the launch's input; any sweep count."""
     cp = C.reference_defaults("cavity")
-    g = C.CavitySolver(cp, device=0, small_solve="off", sweeps_per_launch=spl)
+    g = C.CavitySolver(cp, ordering="rb", device=0, small_solve="off", sweeps_per_launch=spl)
     o = O.Oracle(cp, ordering=O.RB)
     for _ in range(3):
         assert g.step() == o.step()
@@ -131,7 +131,7 @@ def test_tile_stop_inside_launch_and_explicit_sweeps(spl):
 def test_tile_cap_edges(delta):
     """cap = K + delta around the natural stop K of the first solve."""
     cp = C.reference_defaults("channel")
-    g = C.ChannelSolver(cp, device=0, small_solve="off", tuning=TILES)
+    g = C.ChannelSolver(cp, ordering="rb", device=0, small_solve="off", tuning=TILES)
     k, _ = g.step()
     g.close()
     cp2 = C.reference_defaults("channel")
@@ -181,7 +181,7 @@ def test_tile_proof_mode_equals_exact(case, nx, ny, cap, tolf):
 def test_tile_proof_vs_oracle_converging():
     """The reference's 63^2 cavity on proof-mode tiles vs the red-black oracle."""
     cp = C.reference_defaults("cavity")
-    g = C.CavitySolver(cp, device=0, small_solve="off")
+    g = C.CavitySolver(cp, ordering="rb", device=0, small_solve="off")
     o = O.Oracle(cp, ordering=O.RB)
     for _ in range(4):
         assert g.step() == o.step()

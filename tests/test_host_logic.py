@@ -44,7 +44,7 @@ def test_nm_exports_match_header():
 
 
 def test_abi_version():
-    assert _lib.lib().cfd_abi_version() == 8
+    assert _lib.lib().cfd_abi_version() == 9
 
 
 def test_params_struct_layout_matches_header(tmp_path):
@@ -168,10 +168,11 @@ def test_invalid_params_rejected():
 
 
 @pytest.mark.parametrize("case,spl,kw,msg", [
-    ("channel", 3, {}, b"cavity only"), ("channel", 4, {"proof_test": "off"}, b"proof-mode test"),
-    ("cavity", 5, {}, b"sweeps_per_launch"), ("cavity", -1, {}, b"sweeps_per_launch"),
-    ("cavity", 4, {"proof_test": "off"}, b"proof-mode test"),
-    ("cavity", 6, {"ordering": "lex"}, b"sweeps_per_launch"), ("cavity", 5, {}, b"sweeps_per_launch"),
+    ("channel", 3, {"ordering": "rb"}, b"cavity only"),
+    ("channel", 4, {"ordering": "rb", "proof_test": "off"}, b"proof-mode test"),
+    ("cavity", 5, {"ordering": "rb"}, b"sweeps_per_launch"), ("cavity", -1, {}, b"sweeps_per_launch"),
+    ("cavity", 4, {"ordering": "rb", "proof_test": "off"}, b"proof-mode test"),
+    ("cavity", 6, {"ordering": "lex"}, b"sweeps_per_launch"), ("channel", 5, {}, b"sweeps_per_launch"),
     ("channel", 3, {"ordering": "lex"}, b"4 sweeps per launch"),
 ])
 def test_sweeps_per_launch_validated_before_device(case, spl, kw, msg):
@@ -184,6 +185,44 @@ def test_sweeps_per_launch_validated_before_device(case, spl, kw, msg):
     with pytest.raises(_lib.CfdError) as e:
         C.solver_for(C.make_params(case), sweeps_per_launch=spl, **kw)
     assert msg.decode() in str(e.value)
+
+
+def test_reference_order_is_the_default():
+    """cfd_params_init selects the reference's own sweep order (bit-identical
+    output) for the three reference cases; the Python classes take it on one
+    device and red-black on ranks, where the reference order is rejected
+    before any device is touched."""
+    for case in ("cavity", "channel", "backwards_step"):
+        out = _lib.CfdParams()
+        assert _lib.lib().cfd_params_init(C.params.CASE_IDS[case], 0, 0, 0, 0, ctypes.byref(out)) == 0
+        assert out.ordering == _lib.ORDER["lex"]
+    out = _lib.CfdParams()
+    assert _lib.lib().cfd_params_init_rb(0, 0, 0, 0, 0, ctypes.byref(out)) == 0
+    assert out.ordering == _lib.ORDER["rb"]  # (no reference solver: the rank path's order)
+    cp = C.solver.to_cparams(C.make_params("cavity"))
+    assert cp.ordering == _lib.ORDER["lex"]
+    h = _lib.lib().cfd_create_rank(ctypes.byref(cp), 0, 1, 63, None)
+    assert not h
+    assert b"one device" in _lib.lib().cfd_last_error()
+
+
+@pytest.mark.parametrize("case,knob,value", [
+    ("cavity", "march_min_th", 24), ("channel", "march_min_th", 16), ("backwards_step", "march_min_th", 24),
+    ("cavity", "pair_edge_pct", 80), ("channel", "pair_edge_pct", 45), ("backwards_step", "pair_edge_pct", 45),
+    ("cavity", "tile_rounds", 1), ("channel", "tile_rounds", 0), ("rayleigh_benard", "tile_rounds", 1),
+    ("cavity", "tent_th", 64), ("channel", "lexw_edge_pct", 100), ("backwards_step", "lexw_ramp_pct", 0),
+])
+def test_tuning_defaults(case, knob, value):
+    """The launch-plan defaults a solver starts with (cfd_tuning_default, host
+    only): the measured per-case band floors (channel 16 rows, step 24 -
+    profiles/r3_open_groups/tune), boundary-column band lengths, LDS tiles
+    for the cavity only."""
+    cp = C.solver.to_cparams(C.make_params(case))
+    v = ctypes.c_int(-1)
+    assert _lib.lib().cfd_tuning_default(ctypes.byref(cp), _lib.TUNING[knob], ctypes.byref(v)) == 0
+    assert v.value == value
+    assert _lib.lib().cfd_tuning_default(ctypes.byref(cp), _lib.TUNING["pair_wps"], ctypes.byref(v)) != 0
+    assert b"occupancy" in _lib.lib().cfd_last_error()
 
 
 def test_bad_switch_rejected_before_device():
@@ -201,7 +240,7 @@ def test_no_cpu_fallback_without_gpu():
     if probe.stdout.strip() == "True":
         pytest.skip("a GPU is present")
     with pytest.raises(_lib.CfdError):
-        C.CavitySolver(C.make_params("cavity", nx=32))
+        C.CavitySolver(C.make_params("cavity", nx=32), ordering="rb")
 
 
 def test_pvd_writer(tmp_path):
