@@ -381,7 +381,10 @@ __device__ __forceinline__ double proof_ratio_gen(const Coef& c, double tol, dou
 #define CFD_WT_STORE 0
 #endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(double* base, const Geo& g) {
-  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)((size_t)g.nrows * (size_t)g.pitch * sizeof(double)),
+  // num_records is 32 bits: a buffer past 4 GiB is clamped (the host refuses
+  // the CFD_WT_STORE build for such grids: Solver::validate)
+  const size_t bytes = (size_t)g.nrows * (size_t)g.pitch * sizeof(double);
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(unsigned)(bytes < 0xFFFFFFFFull ? bytes : 0xFFFFFFFFull),
                                            0x00020000);
 }
 __device__ __forceinline__ void store_row_pair(double* base, __amdgpu_buffer_rsrc_t r, size_t off, double2 v) {

@@ -465,63 +465,7 @@ __global__ void tol_kernel(Coef c, const double* __restrict__ srcmax, double* __
 
 namespace cfd {
 
-// Sequential sums in the reference's loop order (j outer, i inner, fluid cells),
-// for the bit-identical (lexicographic) mode: mode 0 = sum of the source
-// (channel-01.cpp:622-624, backwards_step-01.cpp fluid cells), mode 1 = kinetic
-// energy 0.5*(u_c^2+v_c^2) (cavity-01.cpp:750-755). The rounding chain is
-// inherently sequential: one wave loads SEQ_PER x 64 terms per round
-// (coalesced, the next round in flight), stages them in LDS and adds them in
-// order from broadcast LDS reads, one dependent add per term. A solid cell contributes
-// -0.0, which leaves every sum unchanged (x + -0.0 == x, -0.0 + -0.0 == -0.0),
-// as skipping it does. Strips are summed in order, each launch continuing from
-// the previous strip's partial sum (accumulate).
-constexpr int SEQ_PER = 8;
-__global__ __launch_bounds__(64) void seq_sum_kernel(Geo g, Coef c, const double* __restrict__ a,
-                                                     const double* __restrict__ b, int mode, double* __restrict__ out,
-                                                     int accumulate) {
-  // one round of 512 terms in LDS, in loop order; the chain reads them back
-  // 16 at a time (every lane the same address: a broadcast) and adds them in
-  // order - no cross-lane moves in the dependent chain
-  __shared__ double buf[64 * SEQ_PER];
-  const int lane = threadIdx.x;
-  const int ja = max(g.j0, 1), jb = min(g.j1, g.ny);
-  const int nx = g.nx;
-  const int n = max(0, jb - ja + 1) * nx;  // cells in loop order: q -> (ja + q / nx, 1 + q % nx) (< 2^31)
-  constexpr int ROUND = 64 * SEQ_PER;
-  auto load = [&](int q0, double (&v)[SEQ_PER]) {  // term q0 + 64 k + lane in v[k]
-#pragma unroll
-    for (int k = 0; k < SEQ_PER; ++k) {
-      const int q = q0 + 64 * k + lane;
-      double t = -0.0;
-      if (q < n) {
-        const int jq = q / nx;
-        const int j = ja + jq, i = 1 + (q - jq * nx);
-        const size_t o = at(g, j, i);
-        const double tv = (mode == 0) ? a[o] : 0.5 * (a[o] * a[o] + b[o] * b[o]);
-        t = is_fluid(c, nx, g.ny, j, i) ? tv : -0.0;
-      }
-      v[k] = t;
-    }
-  };
-  double s = accumulate ? out[0] : 0.0;
-  double v[SEQ_PER], w[SEQ_PER];
-  load(0, v);
-  for (int q0 = 0; q0 < n; q0 += ROUND) {
-    if (q0 + ROUND < n) load(q0 + ROUND, w);  // in flight during the chain
-#pragma unroll
-    for (int k = 0; k < SEQ_PER; ++k) buf[64 * k + lane] = v[k];  // (one wave: LDS ops stay in order)
-    for (int t = 0; t < ROUND; t += 16) {
-      double d[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) d[u] = buf[t + u];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) s += d[u];  // terms past n are -0.0: no change
-    }
-#pragma unroll
-    for (int k = 0; k < SEQ_PER; ++k) v[k] = w[k];
-  }
-  if (lane == 0) out[0] = s;
-}
+// Sequential sums in the reference's loop order: seqsum.hip (seq_sum_launch).
 
 // ------------------------------------------- Poisson, exact lexicographic --
 //

@@ -7,14 +7,18 @@
 namespace cfd {
 
 constexpr int SMLEX_THREADS = 1024;
-constexpr int SMLEX_CELLS = 10048;  // (nx+2)(ny+2) at most: p and its previous values in LDS (157 KiB)
+constexpr int SMLEX_CELLS = 20160;  // (nx+2)(ny+2) at most: p in LDS (157.5 KiB)
+constexpr int SMLEX_MAXC = 5;       // cells of one colour per thread, at most (their state in registers)
 constexpr int SMLEX_NF = 512;       // per-iteration exceedance flags in flight (ring)
 constexpr int SMLEX_NCK = 4;        // checkpoint buffers (global memory, SMLEX_NCK x (nx+2)(ny+2) doubles)
 
-// Grids the kernel takes: p fits the LDS twice, the iterations in flight fit
+// Grids the kernel takes: p fits the LDS, each thread's cells their registers, the iterations in flight fit
 // the flag ring, and the step's block has a corner cell with two fluid
 // neighbours (the same geometries as the multi-block reference-order march).
 bool smlex_fits(const Geo& g, const Coef& c);
+
+// Doubles of checkpoint scratch (ck of smlex_launch) a grid needs.
+size_t smlex_ck_doubles(int nx, int ny);
 
 // Checkpoint spacing (iterations) for a grid: three intervals cover the
 // iterations the first cell runs ahead of the last one.

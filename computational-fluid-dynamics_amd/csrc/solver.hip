@@ -22,6 +22,7 @@
 #include "tile.hpp"
 #include "open.hpp"
 #include "smlex.hpp"
+#include "seqsum.hpp"
 
 namespace cfd {
 
@@ -509,6 +510,11 @@ class Solver {
     if (P.ordering == CFD_ORDER_LEX && P.case_id == CFD_BACKSTEP && !step_lexw_ok() && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
       throw Error(CFD_E_ARG, "lexicographic ordering of a backwards step with a block under 2 cells wide or high "
                              "supports nx + ny < 12000");
+#if CFD_WT_STORE
+    // (write-through p_out stores address a strip's buffer with 32-bit buffer records)
+    if ((double)(P.ny + 2 * HALO + 2) * (double)(((P.nx + 3) + 15) / 16 * 16) * 8.0 >= 4294967295.0)
+      throw Error(CFD_E_ARG, "the CFD_WT_STORE build addresses p buffers below 4 GiB: grid too large");
+#endif
     if (P.case_id == CFD_BACKSTEP && (P.step_i <= 0 || P.step_i >= P.nx))
       throw Error(CFD_E_ARG, "Step location is outside computational domain!");
     if (P.case_id == CFD_BACKSTEP && (P.inlet_jmax < 1 || P.inlet_jmax > P.ny))
@@ -618,7 +624,7 @@ class Solver {
     if (P.case_id != CFD_CAVITY) {
       if (P.ordering == CFD_ORDER_LEX) {  // the reference's sequential sum, bit for bit (strips in order)
         for (size_t q = 0; q < S.size(); ++q)
-          seq_sum_kernel<<<1, 64, 0, st>>>(S[q].g, C, S[q].b[B_F], nullptr, 0, total, q > 0);
+          seq_sum_launch(S[q].g, C, S[q].b[B_F], nullptr, 0, total, q > 0, st);
       } else {
         sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total);
       }
@@ -1379,7 +1385,7 @@ class Solver {
 
   // the reference order on a reference-sized grid in one workgroup (smlex.hip):
   // one strip, no ranks, p fits the LDS twice (small_solve = CFD_OFF: never)
-  double* smlex_ck = nullptr;  // its checkpoints (SMLEX_NCK fields of (nx+2)(ny+2) doubles)
+  double* smlex_ck = nullptr;  // its checkpoints (smlex_ck_doubles)
   bool use_smlex() const {
     return P.ordering == CFD_ORDER_LEX && P.small_solve != CFD_OFF && S.size() == 1 && !comm && smlex_fits(S[0].g, C);
   }
@@ -1390,7 +1396,7 @@ class Solver {
     if (P.case_id == CFD_CAVITY)  // cavity-01.cpp:610-611: each solve starts from a zero field
       HIPC(hipMemsetAsync(X, 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
     if (!smlex_ck)
-      HIPC(hipMalloc(&smlex_ck, (size_t)SMLEX_NCK * (P.nx + 2) * (P.ny + 2) * sizeof(double)));
+      HIPC(hipMalloc(&smlex_ck, smlex_ck_doubles(P.nx, P.ny) * sizeof(double)));
     solve_tolerance();
     int* d_it = stop;
     double* d_res = total + 2;
@@ -1677,7 +1683,7 @@ class Solver {
     }
     if (P.ordering == CFD_ORDER_LEX)
       for (size_t q = 0; q < S.size(); ++q)
-        seq_sum_kernel<<<1, 64, 0, st>>>(S[q].g, C, S[q].b[B_UC], S[q].b[B_VC], 1, total + 1, q > 0);
+        seq_sum_launch(S[q].g, C, S[q].b[B_UC], S[q].b[B_VC], 1, total + 1, q > 0, st);
     else
       sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total + 1);
     check_launch("sum_partials");

@@ -1,5 +1,5 @@
 """The reference's lexicographic SOR order at any grid size on the GPU
-(ordering="lex" for the cavity: csrc/lexw.hpp, the red-black march with the
+(ordering="lex", small_solve="off" for the cavity: csrc/lexw.hpp, the red-black march with the
 i+j time skew), bit for bit against the oracle's restatement of the
 reference's own loop (oracle/ ORC_LEX, pinned to the reference binaries by
 tests/test_oracle_golden.py).
@@ -24,7 +24,7 @@ from test_gpu_parity import assert_bits, ofield  # noqa: E402
 
 
 def solve_both(cp, f, strips=1, spl=0):
-    g = C.CavitySolver(cp, ordering="lex", n_strips=strips, sweeps_per_launch=spl)
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off", n_strips=strips, sweeps_per_launch=spl)
     o = O.Oracle(cp, ordering=O.LEX)
     g.set_field("src", f)
     o.field("src")[...] = f
@@ -67,7 +67,7 @@ def test_converging_solve_stops_at_reference_iteration(spl):
     converges in a few hundred sweeps; the stop is detected up to (nx+ny)/2
     iterations late and replayed to exactly the reference's count."""
     cp = C.reference_defaults("cavity")
-    g = C.CavitySolver(cp, ordering="lex", sweeps_per_launch=spl)
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off", sweeps_per_launch=spl)
     o = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
     g.computeTentativeVelocities()
@@ -88,7 +88,7 @@ def test_whole_steps_bitexact(case):
         cp, steps = C.reference_defaults("cavity"), 12
     else:  # BASELINE configs[0]
         cp, steps = C.make_params("cavity", re=100.0, nx=128, ny=128, dt=1e-3), 8
-    g = C.CavitySolver(cp, ordering="lex")
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off")
     o = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
     for k in range(steps):
@@ -100,7 +100,7 @@ def test_whole_steps_bitexact(case):
 def test_cavity_1024_step_bitexact_capped():
     """BASELINE configs[1] size: whole timesteps in the reference's order."""
     cp = C.make_params("cavity", re=1000.0, nx=1024, ny=1024, max_iters=150)
-    g = C.CavitySolver(cp, ordering="lex")
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off")
     o = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
     for k in range(2):
@@ -109,11 +109,25 @@ def test_cavity_1024_step_bitexact_capped():
         assert_bits(g.field(name), ofield(o, name, cp), f"1024 {name}")
 
 
+def test_cavity_1024_steady_launches_bitexact():
+    """BASELINE configs[1] with the cap past the ramps (K = 1100 > (nx+ny)/2):
+    the steady-state launches (every cell active, poisson_lexw_kernel<*, 4,
+    false, *>) run and the step is bit for bit the reference loop's."""
+    cp = C.make_params("cavity", re=1000.0, nx=1024, ny=1024, max_iters=1100)
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off")
+    o = O.Oracle(cp, ordering=O.LEX)
+    g.applyBoundaryConditions()
+    assert g.step() == o.step()
+    assert g.timing().poisson_steady_launches > 0
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"1024 K=1100 {name}")
+
+
 @pytest.mark.parametrize("spl", [0, 5])
 def test_cavity_4096_step_bitexact_capped(spl):
     """The bench size: one whole timestep in the reference's order (capped)."""
     cp = C.make_params("cavity", re=1000.0, nx=4096, ny=4096, max_iters=24)
-    g = C.CavitySolver(cp, ordering="lex", sweeps_per_launch=spl)
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off", sweeps_per_launch=spl)
     o = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
     assert g.step() == o.step()
@@ -123,7 +137,7 @@ def test_cavity_4096_step_bitexact_capped(spl):
 
 def test_rayleigh_benard_lex_bitexact():
     cp = C.make_params("rayleigh_benard", nx=96, ny=32, ra=2e4, max_iters=300)
-    g = C.RayleighBenardSolver(cp, ordering="lex")
+    g = C.RayleighBenardSolver(cp, ordering="lex", small_solve="off")
     o = O.Oracle(cp, ordering=O.LEX)
     for k in range(6):
         assert g.step() == o.step(), k
@@ -156,7 +170,7 @@ def test_sampled_rows_open_iterations_exact(seed):
     cp = C.make_params("cavity", nx=90, ny=70, max_iters=3000)
     cp.tol_factor = 1e-6
     f = sparse_source(cp, seed)
-    g = C.CavitySolver(cp, ordering="lex")
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off")
     o = O.Oracle(cp, ordering=O.LEX)
     for rep in range(2):
         g.set_field("src", f)
@@ -180,7 +194,7 @@ def random_field(cp, seed, scale=1.0):
 def solve_channel(cp, f, p0, strips=1):
     """One solverPressurePoisson from a given source and initial pressure
     (ghosts included: the reference's first sweep reads them as stored)."""
-    g = C.ChannelSolver(cp, ordering="lex", n_strips=strips)
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off", n_strips=strips)
     o = O.Oracle(cp, ordering=O.LEX)
     g.set_field("src", f)
     g.set_field("p", p0)
@@ -212,7 +226,7 @@ def test_channel_converging_solve_bitexact():
     the sampled rows leave the last iterations open and the exact check / the
     continuation must land on the reference's count."""
     cp = C.reference_defaults("channel")
-    g = C.ChannelSolver(cp, ordering="lex")
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off")
     o = O.Oracle(cp, ordering=O.LEX)
     o.velocity_bc(False)
     for s in (g, ):
@@ -237,7 +251,7 @@ def test_channel_whole_steps_bitexact(case):
         cp, steps = C.reference_defaults("channel"), 12
     else:
         cp, steps = C.make_params("channel", re=1000.0, nx=384, ny=64, max_iters=200), 3
-    g = C.ChannelSolver(cp, ordering="lex")
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off")
     o = O.Oracle(cp, ordering=O.LEX)
     o.velocity_bc(False)
     for k in range(steps):
@@ -250,7 +264,7 @@ def test_channel_4096x512_step_bitexact_capped():
     """BASELINE configs[2] (channel Re=1000, 4096x512): whole timesteps in the
     reference's order, capped, bit for bit."""
     cp = C.make_params("channel", re=1000.0, nx=4096, ny=512, max_iters=30)
-    g = C.ChannelSolver(cp, ordering="lex")
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off")
     o = O.Oracle(cp, ordering=O.LEX)
     o.velocity_bc(False)
     for k in range(2):
@@ -259,10 +273,23 @@ def test_channel_4096x512_step_bitexact_capped():
         assert_bits(g.field(name), ofield(o, name, cp), f"channel 4096x512 {name}")
 
 
+def test_channel_4096x512_steady_launches_bitexact():
+    """BASELINE configs[2] with the cap past the ramps (K = 2320 > (nx+ny)/2):
+    steady-state launches run, bit for bit the reference loop's step."""
+    cp = C.make_params("channel", re=1000.0, nx=4096, ny=512, max_iters=2320)
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off")
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.velocity_bc(False)
+    assert g.step() == o.step()
+    assert g.timing().poisson_steady_launches > 0
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"channel 4096x512 K=2320 {name}")
+
+
 # ---- the backwards step (configs[3]) in the reference's order: lexw.hpp STEP ----
 
 def solve_step(cp, f, p0, strips=1, solves=1):
-    g = C.BackwardsStepSolver(cp, ordering="lex", n_strips=strips)
+    g = C.BackwardsStepSolver(cp, ordering="lex", small_solve="off", n_strips=strips)
     o = O.Oracle(cp, ordering=O.LEX)
     out = []
     for _ in range(solves):
@@ -322,7 +349,7 @@ def test_step_reference_run_bitexact():
     """The reference's own step (256x32) over whole timesteps (the reference
     hits the 10000-sweep cap here from step 2: 3 steps)."""
     cp = C.reference_defaults("backwards_step")
-    g = C.BackwardsStepSolver(cp, ordering="lex")
+    g = C.BackwardsStepSolver(cp, ordering="lex", small_solve="off")
     o = O.Oracle(cp, ordering=O.LEX)
     o.velocity_bc(False)
     for k in range(3):
@@ -335,7 +362,7 @@ def test_step_8192x512_step_bitexact_capped():
     """BASELINE configs[3] (backwards step Re=400, 8192x512) on one device:
     a whole timestep in the reference's order, capped, bit for bit."""
     cp = C.make_params("backwards_step", re=400.0, nx=8192, ny=512, max_iters=24)
-    g = C.BackwardsStepSolver(cp, ordering="lex")
+    g = C.BackwardsStepSolver(cp, ordering="lex", small_solve="off")
     o = O.Oracle(cp, ordering=O.LEX)
     o.velocity_bc(False)
     assert g.step() == o.step()

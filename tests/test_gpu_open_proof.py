@@ -115,3 +115,37 @@ def test_open_proof_full_size_step_capped():
     assert hp == he
     assert_bits(fp["p"], fe["p"], "step 8192x512 p")
     assert tp.proof_fallbacks == 0
+
+
+@pytest.mark.parametrize("case,nx,ny,cap", [("channel", 400, 240, 600), ("backwards_step", 400, 240, 600),
+                                            ("backwards_step", 1600, 160, 400), ("channel", 4096, 512, 200)])
+@pytest.mark.parametrize("strips", [2, 3])
+def test_open_proof_equals_exact_on_strips(case, nx, ny, cap, strips):
+    """The same strip decomposition with and without the proof test: the
+    source and its mean are the same bits, so any difference would come from
+    the 4-sweep proof launch (8 halo rows, refresh timing at strip edges).
+    Iteration counts and fields bit for bit (the step on strips runs 3-sweep
+    proof launches; 1600 wide: its left-of-column tile class)."""
+    cp = C.make_params(case, nx=nx, ny=ny, max_iters=cap)
+    hp, fp, tp = run(case, cp, 2, strips=strips)
+    he, fe, te = run(case, cp, 2, strips=strips, proof_test="off")
+    assert hp == he
+    for n in FIELDS:
+        assert_bits(fp[n], fe[n], f"{case} {nx}x{ny} strips {strips} proof vs exact {n}")
+    assert te.proof_fallbacks == 0
+    assert tp.poisson_sweeps >= 3 * tp.poisson_launches - 3  # proof launches (3-4 sweeps) ran
+
+
+@pytest.mark.parametrize("case,nx,ny,cap", [("channel", 400, 240, 600), ("backwards_step", 1600, 160, 400)])
+@pytest.mark.parametrize("world", [2, 3])
+def test_open_proof_equals_exact_on_ranks(case, nx, ny, cap, world):
+    """Loopback ranks (the rank code path: halo exchange, all-reduced proof
+    slots), proof test on vs off: the same iterations and fields bit for bit."""
+    from test_gpu_ranks import run_ranks
+    cp = C.make_params(case, nx=nx, ny=ny, max_iters=cap)
+    rp = run_ranks(cp, world, 2, small_solve="off", tuning=MARCH)
+    re_ = run_ranks(cp, world, 2, small_solve="off", tuning=MARCH, proof_test="off")
+    for a, b in zip(rp, re_):
+        assert a["its"] == b["its"] and a["rows"] == b["rows"]
+        for n in FIELDS:
+            assert_bits(a[n], b[n], f"{case} rank rows {a['rows']} proof vs exact {n}")
