@@ -99,7 +99,7 @@ __device__ __forceinline__ CavMul cav_mul(const Coef& c, int kind) {
 
 // A cell's register state: W / S as its last update read them
 struct Own {
-  double sw, ss;
+  double sw, ss, pc;  // (pc: its own value, kept while the registers allow: MAXC <= 2)
 };
 
 // LDS layout: row-major, (nx+2) doubles per row (the reference's (j, i)).
@@ -167,7 +167,7 @@ __device__ __forceinline__ double cell_step(const Coef& c, double* P, int* flag,
   bool ex = false;
   const double nv = cell_compute<CASE>(c, s, kind, pc, pE, pN, pW, pS, cav_mul(c, kind), fq, test, tol, ex);
   cell_store<CASE>(P, flag, ck, ncell, b, kind, nv, k, kcap, ex, mlog);
-  s = {pW, pS};
+  s = {pW, pS, nv};
   return nv;
 }
 
@@ -242,13 +242,14 @@ __global__ __launch_bounds__(SMLEX_THREADS) void poisson_smlex_kernel(Geo g, Coe
   // cell: co = kind << 15 | o (o = its LDS index < 2^15; -1: none) and kof,
   // with its iteration at half-sweep H = kbase + (H >> 1) + 2 + kof
   const int jc = c.inlet_jmax + 1, ic = c.step_i;  // the step's block corner (solid)
-  // the cavity's omega / neighbour_count per cell stays in registers while it
-  // fits (up to 2 cells per thread and colour; the indicators are kind bits)
+  // the cavity's multipliers per cell stay in registers while they fit (up to
+  // 2 cells per thread and colour; else from the kind bits at each update)
   constexpr bool PRE = CASE == CAVITY && MAXC <= 2;
+  constexpr bool PCREG = MAXC <= 2;  // the cells' own values in registers
   int co[2][MAXC], kof[2][MAXC];
   double fc[2][FLDS ? 1 : MAXC];
   Own own[2][MAXC];
-  double com[2][PRE ? MAXC : 1];
+  CavMul cm[2][PRE ? MAXC : 1];  // (PRE: the whole multiplier set per cell, small.hpp's PRE)
 #pragma unroll
   for (int col = 0; col < 2; ++col) {
 #pragma unroll
@@ -277,8 +278,8 @@ __global__ __launch_bounds__(SMLEX_THREADS) void poisson_smlex_kernel(Geo g, Coe
       co[col][q] = v;
       kof[col][q] = ko;
       if constexpr (!FLDS) fc[col][FLDS ? 0 : q] = fv;
-      own[col][q] = {0.0, 0.0};
-      if constexpr (PRE) com[col][PRE ? q : 0] = cav_mul(c, kd).om;
+      own[col][q] = {0.0, 0.0, 0.0};
+      if constexpr (PRE) cm[col][PRE ? q : 0] = cav_mul(c, kd);
     }
   }
   // the special thread: B = (jc, ic+1), then the corner, then A = (jc-1, ic)
@@ -298,6 +299,16 @@ __global__ __launch_bounds__(SMLEX_THREADS) void poisson_smlex_kernel(Geo g, Coe
     fB = f[gidx(jc, ic + 1)];
   }
   __syncthreads();
+  auto load_own = [&]() {  // (own values from P: at the start and after a restore)
+    if constexpr (PCREG) {
+#pragma unroll
+      for (int col = 0; col < 2; ++col)
+#pragma unroll
+        for (int q = 0; q < MAXC; ++q)
+          if (co[col][q] >= 0) own[col][q].pc = P[co[col][q] & 0x7fff];
+    }
+  };
+  load_own();
 
   int kbase = 0, kcap = max_iters, K = -1;
   bool replay = false;
@@ -318,7 +329,7 @@ __global__ __launch_bounds__(SMLEX_THREADS) void poisson_smlex_kernel(Geo g, Coe
       // groups of (up to) two cells: the neighbours of both first (the cells
       // of one colour never read each other: the loads of both in flight
       // together), then the arithmetic, then the stores
-      constexpr int G = (CASE != CHANNEL && MAXC >= 4) ? 1 : 2;
+      constexpr int G = (CASE == CAVITY || (CASE == BACKSTEP && MAXC >= 4)) ? 1 : 2;
 #pragma unroll
       for (int q0 = 0; q0 < MAXC; q0 += G) {
         double pc[G], pE[G], pN[G], pW[G], pS[G], fq[G], nv[G];
@@ -329,12 +340,14 @@ __global__ __launch_bounds__(SMLEX_THREADS) void poisson_smlex_kernel(Geo g, Coe
         for (int u = 0; u < G; ++u) {
           const int q = q0 + u < MAXC ? q0 + u : MAXC - 1;
           int v = (q0 + u < MAXC) ? co[cc][q] : -1;
-          asm volatile("" : "+v"(v));  // (keeps the values derived here out of the loop: registers)
+          // (more than 2 cells per thread and colour: the values derived here are
+          // kept out of the loop, where they would hold registers)
+          if constexpr (!PCREG) asm volatile("" : "+v"(v));
           kq[u] = hk + kof[cc][q];
           act[u] = v >= 0 && kq[u] > kbase && kq[u] <= kcap;
           kd[u] = v >> 15;
           bq[u] = nbrs_o(L, act[u] ? (v & 0x7fff) : W + 1);  // (an inactive slot loads a harmless cell)
-          pc[u] = P[bq[u].o];
+          pc[u] = PCREG ? own[cc][q].pc : P[bq[u].o];
           pE[u] = P[bq[u].e];
           pN[u] = P[bq[u].n];
           pW[u] = P[bq[u].w];
@@ -346,10 +359,7 @@ __global__ __launch_bounds__(SMLEX_THREADS) void poisson_smlex_kernel(Geo g, Coe
           const int q = q0 + u < MAXC ? q0 + u : MAXC - 1;
           ex[u] = false;
           CavMul m{};
-          if (CASE == CAVITY) {
-            m = cav_mul(c, kd[u]);
-            if (PRE) m.om = com[cc][PRE ? q : 0];
-          }
+          if (CASE == CAVITY) m = PRE ? cm[cc][PRE ? q : 0] : cav_mul(c, kd[u]);
           nv[u] = cell_compute<CASE>(c, own[cc][q], kd[u], pc[u], pE[u], pN[u], pW[u], pS[u], m, fq[u],
                                      !replay && kq[u] >= 2, tol, ex[u]);
         }
@@ -358,7 +368,7 @@ __global__ __launch_bounds__(SMLEX_THREADS) void poisson_smlex_kernel(Geo g, Coe
           const int q = q0 + u < MAXC ? q0 + u : MAXC - 1;
           if (act[u] && q0 + u < MAXC) {
             cell_store<CASE>(P, flag, ck, ncell, bq[u], kd[u], nv[u], kq[u], kcap, ex[u], ml);
-            own[cc][q] = {pW[u], pS[u]};
+            own[cc][q] = {pW[u], pS[u], nv[u]};
           }
         }
       }
@@ -418,6 +428,7 @@ __global__ __launch_bounds__(SMLEX_THREADS) void poisson_smlex_kernel(Geo g, Coe
       __syncthreads();
       refresh_all<CASE>(c, nx, ny, L, P);  // the field after iteration mstar's refresh
     }
+    load_own();
     kbase = mstar;
     kcap = K;
     replay = true;

@@ -133,7 +133,7 @@ def test_open_proof_equals_exact_on_strips(case, nx, ny, cap, strips):
     for n in FIELDS:
         assert_bits(fp[n], fe[n], f"{case} {nx}x{ny} strips {strips} proof vs exact {n}")
     assert te.proof_fallbacks == 0
-    assert tp.poisson_sweeps >= 3 * tp.poisson_launches - 3  # proof launches (3-4 sweeps) ran
+    assert tp.poisson_sweeps > 2.5 * tp.poisson_launches  # proof launches (3-4 sweeps) ran
 
 
 @pytest.mark.parametrize("case,nx,ny,cap", [("channel", 400, 240, 600), ("backwards_step", 1600, 160, 400)])
