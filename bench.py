@@ -159,7 +159,7 @@ def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch
             "steady_launch_us": round(steady_ms * 1e3, 2) if tm.poisson_steady_launches else None,
             "steady_achieved_GBs": round(achieved, 1) if achieved else None,
             "steady_frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "steady_traffic": pmc_traffic(f"r3_pmc_{args.case}_lex_{cp.nx}x{cells_per_launch // (cp.nx + 2) - 2}.json",
+            "steady_traffic": pmc_traffic(f"r4_pmc_{args.case}_lex_{cp.nx}x{cells_per_launch // (cp.nx + 2) - 2}.json",
                                           cp.nx, cells_per_launch // (cp.nx + 2),
                                           round(tm.poisson_sweeps / max(tm.poisson_launches, 1)))}
 
@@ -369,7 +369,7 @@ def run(args, rank: int, world: int, local_rank: int, comm, group, loopback: boo
         # (the unfused algorithm's traffic): the temporal-blocking gain
         effective = achieved * sweeps_per_launch
         # HBM bytes per launch from the committed PMC pass of the same workload (profiles/)
-        traffic = pmc_traffic(f"r3_pmc_{args.case}_{args.ordering}_{cp.nx}x{wrows - 2}.json", cp.nx, wrows,
+        traffic = pmc_traffic(f"r4_pmc_{args.case}_{args.ordering}_{cp.nx}x{wrows - 2}.json", cp.nx, wrows,
                               round(sweeps_per_launch))
         mlups = updates / elapsed / 1e6
         kcase = kcase_of(args.case)

@@ -11,4 +11,5 @@ want() { [ -z "$CASES" ] || [[ " $CASES " == *" $1 "* ]]; }
 { ! want ch || CASE=channel NX=4096 NY=512 ORDER=rb KSUB="poisson_open_proof_kernel<1, 4>" SPL=4 PMC_ITERS=400 bash $P; } &&
 { ! want st || CASE=backwards_step NX=8192 NY=512 RE=400 ORDER=rb KSUB="poisson_open_proof_kernel<2, 4>" SPL=4 PMC_ITERS=400 bash $P; } &&
 { ! want chlex || CASE=channel NX=4096 NY=512 ORDER=lex KSUB="poisson_lexw_kernel<1, 4, false, true>" SPL=4 PMC_ITERS=3000 bash $P; } &&
+{ ! want stlex || CASE=backwards_step NX=8192 NY=512 RE=400 ORDER=lex KSUB="poisson_lexw_kernel<2, 4, false, true>" SPL=4 PMC_ITERS=5000 bash $P; } &&
 { ! want cav4klex || CASE=cavity NX=4096 NY=4096 ORDER=lex KSUB="poisson_lexw_kernel<0, 4, false, true>" SPL=4 PMC_ITERS=5000 bash $P; }
