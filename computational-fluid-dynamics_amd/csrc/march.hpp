@@ -953,9 +953,16 @@ __global__ __launch_bounds__(256, PROOF ? CFD_PROOF_MIN_WAVES : (CASE == CAVITY)
     const int nci = pl.ctiles - ned;
     if (t >= nci * nbi) return;
     // column tiles of one band side by side: their shared halo columns are
-    // read at the same moment on the same XCD (one L2)
-    ctile = 1 + t % nci;
-    band = t / nci;
+    // read at the same moment on the same XCD (one L2); flags bit 3: the bands
+    // of one column tile one after another instead (their shared halo rows on
+    // one XCD)
+    if (flags & 8) {
+      ctile = 1 + t / nbi;
+      band = t % nbi;
+    } else {
+      ctile = 1 + t % nci;
+      band = t / nci;
+    }
     // skip the mixed tiles (cxa < cxb, both inside 1 .. ctiles-2)
     if (pl.cxa > 0 && ctile >= pl.cxa - 1) ++ctile;
     if (pl.cxb > 0 && ctile >= pl.cxb - 1) ++ctile;

@@ -195,7 +195,7 @@ class Solver {
   int resident_waves = 2048;  // wave-march tiles in flight (CUs x 4 SIMDs x waves per SIMD)
   int resident_pair_waves = 2048;  // the same for the two-iteration kernel
   int pair_edge_pct = 45;          // boundary-column band length, % of the interior march (open cases; cavity: 80)
-  int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order
+  int march_flags = 3;         // bit 0 alternate directions, bit 1 XCD-aware order, bit 3 column-major tile order
   int march_min_th = MARCH_MIN_TH;
   int tent_th = 64;            // rows per band of the predictor's march
   int n_cu = 256;              // compute units of the device
@@ -216,6 +216,7 @@ class Solver {
       case CFD_TUNE_TENT_TH: tent_th = std::max(4, v); break;
       case CFD_TUNE_LEXW_RAMP_PCT: lexw_ramp_pct = std::max(0, std::min(100, v)); break;
       case CFD_TUNE_TILE_ROUNDS: tile_rounds = std::max(0, std::min(v, 16)); break;
+      case CFD_TUNE_MARCH_ORDER: march_flags = (march_flags & ~8) | (v ? 8 : 0); break;
       default: throw Error(CFD_E_ARG, "unknown tuning knob");
     }
   }
@@ -301,7 +302,7 @@ class Solver {
       // indicators), the open cases 45 %; band floor 16 rows for the channel,
       // 24 otherwise; LDS tiles for the cavity only
       for (int knob : {CFD_TUNE_LEXW_EDGE_PCT, CFD_TUNE_PAIR_EDGE_PCT, CFD_TUNE_MARCH_MIN_TH, CFD_TUNE_TENT_TH,
-                       CFD_TUNE_LEXW_RAMP_PCT, CFD_TUNE_TILE_ROUNDS}) {
+                       CFD_TUNE_LEXW_RAMP_PCT, CFD_TUNE_TILE_ROUNDS, CFD_TUNE_MARCH_ORDER}) {
         int v = 0;
         if (cfd_tuning_default(&P, knob, &v) == CFD_OK) set_tuning_value(knob, v);
       }

@@ -217,9 +217,11 @@ enum cfd_tuning {
                                  24 otherwise) */
   CFD_TUNE_TENT_TH = 6,       /* rows per band of the predictor's march (>= 4) */
   CFD_TUNE_LEXW_RAMP_PCT = 7, /* lexicographic ramp launches: band height floor, % of the steady plan's (0..100) */
-  CFD_TUNE_TILE_ROUNDS = 8    /* red-black, one strip: LDS-tile launches when the grid fits this many
+  CFD_TUNE_TILE_ROUNDS = 8,   /* red-black, one strip: LDS-tile launches when the grid fits this many
                                  resident rounds of tiles (one per CU; 0: never, the march launches;
                                  default 1 for the cavity, 0 for the open cases) */
+  CFD_TUNE_MARCH_ORDER = 9    /* red-black march launches: 0 = the column tiles of a band on consecutive waves
+                                 (default), 1 = the bands of a column tile (ABI 9) */
 };
 int cfd_set_tuning(cfd_solver* s, int knob, int value);
 /* The default a solver created from these parameters starts with (host only, no

@@ -11,7 +11,7 @@ TAG=${TAG:-${CASE}_${ORDER}_${NX}x${NY}}
 D=gpurun_out/prof/$TAG
 mkdir -p $D
 export TMPDIR=/tmp
-A="--case $CASE --nx $NX --ny $NY --re ${RE:-1000} --ordering $ORDER --no-cpu-baseline --lex-steps 0"
+A="--case $CASE --nx $NX --ny $NY --re ${RE:-1000} --ordering $ORDER --no-cpu-baseline --lex-steps 0 ${EXTRA}"
 W="--warmup ${PMC_WARMUP:-1}"  # (the first step: source in the lid corners only, not the steady state)
 timeout -k 10 300 python3 -u bench.py $A --steps ${STEPS:-2} --warmup 1 > $D/bench.json 2> $D/bench.err
 rc=$?; echo "bench exit $rc"; cat $D/bench.json; [ $rc -ne 0 ] && { tail -5 $D/bench.err; exit $rc; }
