@@ -153,8 +153,9 @@ extern "C" int cfd_params_init_rb(double ra, double pr, int nx, int ny, double d
 // Launch-plan defaults that do not depend on the device (include/cfd_amd.h
 // cfd_tuning_default); Solver::init starts from these. Measured on MI355X
 // (DESIGN.md §4): cavity boundary-column bands 80 % of the interior march (open
-// cases 45 %); the channel's proof march fastest at a 16-row band floor, the
-// step's (and the cavity's) at 24; LDS tiles for the cavity only.
+// cases 45 %); a 16-row band floor for the channel and for every reference-order
+// (lexw) march, 24 for the red-black step and cavity marches
+// (profiles/r4_tune); LDS tiles for the cavity only.
 extern "C" int cfd_tuning_default(const cfd_params* p, int knob, int* value) {
   if (!p || !value) {
     cfd::set_last_error("null argument");
@@ -164,7 +165,7 @@ extern "C" int cfd_tuning_default(const cfd_params* p, int knob, int* value) {
   switch (knob) {
     case CFD_TUNE_LEXW_EDGE_PCT: *value = 100; return CFD_OK;
     case CFD_TUNE_PAIR_EDGE_PCT: *value = cav ? 80 : 45; return CFD_OK;
-    case CFD_TUNE_MARCH_MIN_TH: *value = p->case_id == CFD_CHANNEL ? 16 : 24; return CFD_OK;
+    case CFD_TUNE_MARCH_MIN_TH: *value = (p->case_id == CFD_CHANNEL || p->ordering == CFD_ORDER_LEX) ? 16 : 24; return CFD_OK;
     case CFD_TUNE_TENT_TH: *value = 64; return CFD_OK;
     case CFD_TUNE_LEXW_RAMP_PCT: *value = 0; return CFD_OK;
     case CFD_TUNE_TILE_ROUNDS: *value = cav ? 1 : 0; return CFD_OK;

@@ -207,17 +207,20 @@ def test_reference_order_is_the_default():
 
 
 @pytest.mark.parametrize("case,knob,value", [
-    ("cavity", "march_min_th", 24), ("channel", "march_min_th", 16), ("backwards_step", "march_min_th", 24),
+    ("cavity", "march_min_th", 16), ("channel", "march_min_th", 16), ("backwards_step", "march_min_th", 16),
+    ("cavity/rb", "march_min_th", 24), ("channel/rb", "march_min_th", 16), ("backwards_step/rb", "march_min_th", 24),
     ("cavity", "pair_edge_pct", 80), ("channel", "pair_edge_pct", 45), ("backwards_step", "pair_edge_pct", 45),
     ("cavity", "tile_rounds", 1), ("channel", "tile_rounds", 0), ("rayleigh_benard", "tile_rounds", 1),
     ("cavity", "tent_th", 64), ("channel", "lexw_edge_pct", 100), ("backwards_step", "lexw_ramp_pct", 0),
 ])
 def test_tuning_defaults(case, knob, value):
     """The launch-plan defaults a solver starts with (cfd_tuning_default, host
-    only): the measured per-case band floors (channel 16 rows, step 24 -
-    profiles/r3_open_groups/tune), boundary-column band lengths, LDS tiles
-    for the cavity only."""
-    cp = C.solver.to_cparams(C.make_params(case))
+    only): the measured band floors (16 rows for the channel and every
+    reference-order march, 24 for the red-black step and cavity -
+    profiles/r4_tune), boundary-column band lengths, LDS tiles for the
+    cavity only."""
+    case, _, order = case.partition("/")
+    cp = C.solver.to_cparams(C.make_params(case), ordering=order or "lex")
     v = ctypes.c_int(-1)
     assert _lib.lib().cfd_tuning_default(ctypes.byref(cp), _lib.TUNING[knob], ctypes.byref(v)) == 0
     assert v.value == value
