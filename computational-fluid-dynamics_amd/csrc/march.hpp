@@ -676,31 +676,56 @@ __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const dou
 #undef CFD_N
 }
 
+// The first two groups of 10 march steps of an interior wave (GST = the step
+// index 0..19 at compile time; p = the parity alignment step, 0 or 1) skip the
+// red / black updates of sweep S whose rows lie outside the dependency cone of
+// the band's output rows [y0, y1): sweep S is needed on rows
+// [y0 - 2(NS-1-S) - 1, ...) (red) and [y0 - 2(NS-1-S), ...) (black), which the
+// front reaches at step 3 + 4S + p (red) / 5 + 4S + p (black). Rows outside the
+// cone are never read by a needed update (red(S+1) at r reads black(S) at
+// r-1..r+1, black(S) reads red(S) likewise), so the stored rows and the proof
+// ratios (black rows inside [y0, y1) only) are the same bits (exact-residual
+// launches: the residuals of rows [y0, y1) read one row further, so every
+// threshold is one step earlier); the skipped
+// updates are ~10 % of an interior wave's VALU work (80 of 8 x (th + 19)
+// half-row updates at th = 81). The drain end has no such rows: the cone
+// reaches past y1 exactly as far as the pipeline lags the front.
+template <int GST, int T>
+__device__ __forceinline__ bool cone_step(int p) {
+  if constexpr (GST < 0 || GST > T) return true;
+  else if constexpr (GST < T) return false;
+  else return p == 0;
+}
+
 // sweeps S .. NS-1 of one march step (compile-time recursion over the sweeps)
-template <int S, int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF, bool RC>
-__device__ __forceinline__ void cav_sweeps(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R) {
+template <int S, int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF, bool RC, int GST = -1>
+__device__ __forceinline__ void cav_sweeps(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R, int p = 0) {
   if constexpr (S < NS) {
     // red at R-(2S+1)d (parity PAR^1), black at R-(2S+2)d (PAR), residual at R-(2S+3)d
-    cav_update<DIR, ROT, PAR ^ 1, 0, EDGE, false, RC>(x, s.w[S], R - (2 * S + 1) * DIR, 2 * S + 1,
-                                                      s.fr[CFD_S10(2 * S + 1)]);
-    if constexpr (PROOF && !EDGE) {
-      const int jb = R - (2 * S + 2) * DIR;
-      const double wgt = (jb >= x.py0 && jb < x.py1) ? 1.0 : 0.0;  // row-uniform
-      cav_update<DIR, ROT, PAR, 1, EDGE, true, RC>(x, s.w[S], jb, 2 * S + 2, s.fr[CFD_S10(2 * S + 2)], wgt,
-                                                   &s.rmax[S]);
-    } else {
-      cav_update<DIR, ROT, PAR, 1, EDGE, false, RC>(x, s.w[S], R - (2 * S + 2) * DIR, 2 * S + 2,
-                                                    s.fr[CFD_S10(2 * S + 2)]);
+    constexpr int sh = PROOF ? 0 : 1;  // (exact residuals of rows [y0, y1) read rows y0-1 / y1: one row more)
+    if (cone_step<GST, 3 + 4 * S - sh>(p))
+      cav_update<DIR, ROT, PAR ^ 1, 0, EDGE, false, RC>(x, s.w[S], R - (2 * S + 1) * DIR, 2 * S + 1,
+                                                        s.fr[CFD_S10(2 * S + 1)]);
+    if (cone_step<GST, 5 + 4 * S - sh>(p)) {
+      if constexpr (PROOF && !EDGE) {
+        const int jb = R - (2 * S + 2) * DIR;
+        const double wgt = (jb >= x.py0 && jb < x.py1) ? 1.0 : 0.0;  // row-uniform
+        cav_update<DIR, ROT, PAR, 1, EDGE, true, RC>(x, s.w[S], jb, 2 * S + 2, s.fr[CFD_S10(2 * S + 2)], wgt,
+                                                     &s.rmax[S]);
+      } else {
+        cav_update<DIR, ROT, PAR, 1, EDGE, false, RC>(x, s.w[S], R - (2 * S + 2) * DIR, 2 * S + 2,
+                                                      s.fr[CFD_S10(2 * S + 2)]);
+      }
     }
     cav_residual<DIR, ROT, EDGE, PROOF>(x, s.w[S], R - (2 * S + 3) * DIR, 2 * S + 3, s.fr[CFD_S10(2 * S + 3)],
                                         S == NS - 1, s.rmax[S]);
     if constexpr (S + 1 < NS) s.w[S + 1][CFD_SLOT(2 * S + 2)] = s.w[S][CFD_SLOT(2 * S + 2)];
-    cav_sweeps<S + 1, NS, DIR, ROT, PAR, EDGE, PROOF, RC>(x, s, R);
+    cav_sweeps<S + 1, NS, DIR, ROT, PAR, EDGE, PROOF, RC, GST>(x, s, R, p);
   }
 }
 
-template <int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF, int PD, bool RC>  // PAR = parity of R
-__device__ __forceinline__ void cav_step(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R) {
+template <int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF, int PD, bool RC, int GST = -1>  // PAR = parity of R
+__device__ __forceinline__ void cav_step(const WaveCtx<CAVITY>& x, CavRun<NS>& s, int R, int p = 0) {
   s.w[0][CFD_SLOT(0)] = s.np[CFD_S10(0)];
   s.fr[CFD_S10(1)] = s.nf[CFD_S10(1)];
   if constexpr (PROOF && !EDGE) {  // the proof's Pin: every p_in value this wave uses
@@ -714,7 +739,7 @@ __device__ __forceinline__ void cav_step(const WaveCtx<CAVITY>& x, CavRun<NS>& s
     s.np[CFD_S10(-PD)] = x.ld_fast(x.pin, R + PD * DIR);
     s.nf[CFD_S10(1 - PD)] = x.ld_fast(x.f, R + (PD - 1) * DIR);
   }
-  cav_sweeps<0, NS, DIR, ROT, PAR, EDGE, PROOF, RC>(x, s, R);
+  cav_sweeps<0, NS, DIR, ROT, PAR, EDGE, PROOF, RC, GST>(x, s, R, p);
 }
 
 // 1: the cavity's proof-mode bands near the top / bottom rows and the
@@ -723,6 +748,11 @@ __device__ __forceinline__ void cav_step(const WaveCtx<CAVITY>& x, CavRun<NS>& s
 // launch is balanced - per-wave stamps, profiles/r3_balance/ - so it stays off)
 #ifndef CFD_CAV_GROUPS
 #define CFD_CAV_GROUPS 0
+#endif
+// 1: interior waves skip the updates outside their band's dependency cone in
+// the first 20 march steps (cav_sweeps)
+#ifndef CFD_CAV_CONE
+#define CFD_CAV_CONE 1
 #endif
 // PROOF: r[q] = max |black update| of sweep q over the output cells
 // (interior waves; 0 on boundary-column waves), pm = max |p_in| loaded.
@@ -759,8 +789,40 @@ __device__ __forceinline__ void cav_march(const WaveCtx<CAVITY>& x0, int y0, int
     }
   }
   int R = Rbeg;
+  int st = 0;
+#if CFD_CAV_CONE
+  if constexpr (!EDGE) {  // the first two groups: updates outside the band's cone skipped (cav_sweeps)
+    const int p = Rb0 & 1;
+    cav_step<NS, DIR, 0, 0, EDGE, PROOF, PD, RC, 0>(x, s, R, p);
+    cav_step<NS, DIR, 1, 1, EDGE, PROOF, PD, RC, 1>(x, s, R + DIR, p);
+    cav_step<NS, DIR, 2, 0, EDGE, PROOF, PD, RC, 2>(x, s, R + 2 * DIR, p);
+    cav_step<NS, DIR, 3, 1, EDGE, PROOF, PD, RC, 3>(x, s, R + 3 * DIR, p);
+    cav_step<NS, DIR, 4, 0, EDGE, PROOF, PD, RC, 4>(x, s, R + 4 * DIR, p);
+    cav_step<NS, DIR, 0, 1, EDGE, PROOF, PD, RC, 5>(x, s, R + 5 * DIR, p);
+    cav_step<NS, DIR, 1, 0, EDGE, PROOF, PD, RC, 6>(x, s, R + 6 * DIR, p);
+    cav_step<NS, DIR, 2, 1, EDGE, PROOF, PD, RC, 7>(x, s, R + 7 * DIR, p);
+    cav_step<NS, DIR, 3, 0, EDGE, PROOF, PD, RC, 8>(x, s, R + 8 * DIR, p);
+    cav_step<NS, DIR, 4, 1, EDGE, PROOF, PD, RC, 9>(x, s, R + 9 * DIR, p);
+    st += 10;
+    R += 10 * DIR;
+    if (nsteps > 10) {
+      cav_step<NS, DIR, 0, 0, EDGE, PROOF, PD, RC, 10>(x, s, R, p);
+      cav_step<NS, DIR, 1, 1, EDGE, PROOF, PD, RC, 11>(x, s, R + DIR, p);
+      cav_step<NS, DIR, 2, 0, EDGE, PROOF, PD, RC, 12>(x, s, R + 2 * DIR, p);
+      cav_step<NS, DIR, 3, 1, EDGE, PROOF, PD, RC, 13>(x, s, R + 3 * DIR, p);
+      cav_step<NS, DIR, 4, 0, EDGE, PROOF, PD, RC, 14>(x, s, R + 4 * DIR, p);
+      cav_step<NS, DIR, 0, 1, EDGE, PROOF, PD, RC, 15>(x, s, R + 5 * DIR, p);
+      cav_step<NS, DIR, 1, 0, EDGE, PROOF, PD, RC, 16>(x, s, R + 6 * DIR, p);
+      cav_step<NS, DIR, 2, 1, EDGE, PROOF, PD, RC, 17>(x, s, R + 7 * DIR, p);
+      cav_step<NS, DIR, 3, 0, EDGE, PROOF, PD, RC, 18>(x, s, R + 8 * DIR, p);
+      cav_step<NS, DIR, 4, 1, EDGE, PROOF, PD, RC, 19>(x, s, R + 9 * DIR, p);
+      st += 10;
+      R += 10 * DIR;
+    }
+  }
+#endif
   constexpr int BACK = 2 * NS + 5;  // rows behind the front a step touches (+1)
-  for (int st = 0; st < nsteps; st += 10, R += 10 * DIR) {
+  for (; st < nsteps; st += 10, R += 10 * DIR) {
 #if CFD_CAV_GROUPS
     const int glo = (DIR > 0) ? R - BACK : R - 11, ghi = (DIR > 0) ? R + 11 : R + BACK;
     if (RC && glo > gmin && ghi < gmax) {  // (wave-uniform)
