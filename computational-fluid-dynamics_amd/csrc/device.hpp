@@ -400,4 +400,15 @@ __device__ __forceinline__ void store_row_pair(double* base, __amdgpu_buffer_rsr
 #endif
 }
 
+// Whether march step GST (0..19: the first two groups of a wave's march; -1:
+// a later step) runs an update whose rows enter the band's dependency cone at
+// step T + p (p: the march's parity alignment step, 0 or 1): compile-time
+// except at step T itself (march.hpp cav_sweeps, lexw.hpp lx_sweeps).
+template <int GST, int T>
+__device__ __forceinline__ bool cone_step(int p) {
+  if constexpr (GST < 0 || GST > T) return true;
+  else if constexpr (GST < T) return false;
+  else return p == 0;
+}
+
 }  // namespace cfd

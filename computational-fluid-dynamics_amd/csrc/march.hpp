@@ -689,13 +689,8 @@ __device__ __forceinline__ void cav_residual(const WaveCtx<CAVITY>& x, const dou
 // threshold is one step earlier); the skipped
 // updates are ~10 % of an interior wave's VALU work (80 of 8 x (th + 19)
 // half-row updates at th = 81). The drain end has no such rows: the cone
-// reaches past y1 exactly as far as the pipeline lags the front.
-template <int GST, int T>
-__device__ __forceinline__ bool cone_step(int p) {
-  if constexpr (GST < 0 || GST > T) return true;
-  else if constexpr (GST < T) return false;
-  else return p == 0;
-}
+// reaches past y1 exactly as far as the pipeline lags the front. (cone_step:
+// device.hpp)
 
 // sweeps S .. NS-1 of one march step (compile-time recursion over the sweeps)
 template <int S, int NS, int DIR, int ROT, int PAR, bool EDGE, bool PROOF, bool RC, int GST = -1>
