@@ -51,6 +51,11 @@ __device__ __forceinline__ bool tile_refreshes(const Coef& c, int nx, int ny, in
 #ifndef CFD_TILE_STAMPS
 #define CFD_TILE_STAMPS 0
 #endif
+// 1: the cavity's sweeps skip the region rows outside the dependency cone of
+// the owned rows (the open cases' refresh widens their cone: all rows)
+#ifndef CFD_TILE_CONE
+#define CFD_TILE_CONE 1
+#endif
 #if CFD_TILE_STAMPS
 constexpr int STAMP_SEGS = 8;
 __device__ unsigned long long tile_stamp_buf[1024 * TILE_WAVES * STAMP_SEGS];
@@ -226,6 +231,14 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
         if (r0 < RH) Cv = P[r0 * 64 + lane];
       }
       const int rb = phase_rows();
+      // cavity: region rows inside the dependency cone of what the launch
+      // evaluates (owned rows TILE_H .. RH-TILE_H-1 after nsw sweeps; black of
+      // sweep s reaches 2(nsw-1-s) rows beyond them, red one more, exact
+      // residuals read one row further): the rows outside never feed an owned
+      // cell, a proving cell or a residual (same bits, fewer row updates)
+      const int dist = 2 * (nsw - 1 - s) + (col == 0 ? 1 : 0) + (PROOF ? 0 : 1);
+      const int clo = (CASE == CAVITY && CFD_TILE_CONE) ? max(1, TILE_H - dist) : 1;
+      const int chi = (CASE == CAVITY && CFD_TILE_CONE) ? min(RH - 2, RH - 1 - TILE_H + dist) : RH - 2;
 #pragma unroll
       for (int q = 0; q < TILE_RPW; ++q) {
         const int r = prow_q(rb, q);
@@ -240,7 +253,7 @@ __global__ __launch_bounds__(TILE_WAVES * 64) void poisson_tile_kernel(Geo g, Co
           ld3(r, C, S, N);
         }
         // region rows with both neighbours in LDS, grid rows that are updated
-        if (r >= 1 && r <= RH - 2 && j >= 1 && j <= ny && j > rmin && j < rmax) {
+        if (r >= clo && r <= chi && j >= 1 && j <= ny && j > rmin && j < rmax) {
           const bool open = CASE != BACKSTEP || j <= c.inlet_jmax;  // (row-uniform) the step's block rows: j > jmax
           const bool top = j == ny;
           // proof mode, black half-sweep: this row's cells prove (row-uniform part)
