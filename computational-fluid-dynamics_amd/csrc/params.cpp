@@ -154,8 +154,10 @@ extern "C" int cfd_params_init_rb(double ra, double pr, int nx, int ny, double d
 // cfd_tuning_default); Solver::init starts from these. Measured on MI355X
 // (DESIGN.md §4): cavity boundary-column bands 80 % of the interior march (open
 // cases 45 %); a 16-row band floor for the channel and for every reference-order
-// (lexw) march, 24 for the red-black step and cavity marches
-// (profiles/r4_tune); LDS tiles for the cavity only.
+// (lexw) march, 24 for the red-black step and cavity marches; reference-order
+// wall-tile bands 75 % of the interior band up to 2048 rows, 100 % above
+// (channel 160 -> 169, cavity 1024^2 160 -> 178 GLUPS; 4096^2 best at 100:
+// profiles/r4_tune); LDS tiles for the cavity only.
 extern "C" int cfd_tuning_default(const cfd_params* p, int knob, int* value) {
   if (!p || !value) {
     cfd::set_last_error("null argument");
@@ -163,7 +165,7 @@ extern "C" int cfd_tuning_default(const cfd_params* p, int knob, int* value) {
   }
   const bool cav = p->case_id == CFD_CAVITY || p->case_id == CFD_RAYLEIGH_BENARD;
   switch (knob) {
-    case CFD_TUNE_LEXW_EDGE_PCT: *value = 100; return CFD_OK;
+    case CFD_TUNE_LEXW_EDGE_PCT: *value = p->ny <= 2048 ? 75 : 100; return CFD_OK;
     case CFD_TUNE_PAIR_EDGE_PCT: *value = cav ? 80 : 45; return CFD_OK;
     case CFD_TUNE_MARCH_MIN_TH: *value = (p->case_id == CFD_CHANNEL || p->ordering == CFD_ORDER_LEX) ? 16 : 24; return CFD_OK;
     case CFD_TUNE_TENT_TH: *value = 64; return CFD_OK;

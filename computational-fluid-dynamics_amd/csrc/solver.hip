@@ -229,7 +229,7 @@ class Solver {
   double* resmax = nullptr;
   hipEvent_t ev_f0 = nullptr, ev_f1 = nullptr;
   int resident_lexw_waves = 2048;
-  int lexw_edge_pct = 100;  // wall-tile bands as long as interior ones (measured at 4096^2; CFD_LEXW_EDGE_PCT)
+  int lexw_edge_pct = 100;  // wall-tile band length, % of the interior band (cfd_tuning_default: 75 up to 2048 rows)
   int lexw_ramp_pct = 0;    // ramp launches: bands at least this % of the steady plan's (CFD_TUNE_LEXW_RAMP_PCT)
   // the multi-block reference-order march (lexw.hpp): cavity (1-4 sweeps per
   // launch), channel and backwards step (4; 3 on strips). The step's solid

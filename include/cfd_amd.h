@@ -211,7 +211,8 @@ enum cfd_tuning {
   CFD_TUNE_PAIR_WPS = 0,      /* waves per SIMD the fused red-black launch is planned for (1..4) */
   CFD_TUNE_WAVE_WPS = 1,      /* the same for the one-sweep launch */
   CFD_TUNE_LEXW_WAVES = 2,    /* tiles per lexicographic-order launch (>= 64) */
-  CFD_TUNE_LEXW_EDGE_PCT = 3, /* wall-tile band length, % of the interior band (10..100) */
+  CFD_TUNE_LEXW_EDGE_PCT = 3, /* wall-tile band length, % of the interior band (10..100; default 75 up to
+                                 2048 rows, 100 above) */
   CFD_TUNE_PAIR_EDGE_PCT = 4, /* boundary-column band length of red-black launches, % (10..100) */
   CFD_TUNE_MARCH_MIN_TH = 5,  /* minimum rows per band of a march launch (>= 1; default 16 for the channel,
                                  24 otherwise) */

@@ -211,16 +211,19 @@ def test_reference_order_is_the_default():
     ("cavity/rb", "march_min_th", 24), ("channel/rb", "march_min_th", 16), ("backwards_step/rb", "march_min_th", 24),
     ("cavity", "pair_edge_pct", 80), ("channel", "pair_edge_pct", 45), ("backwards_step", "pair_edge_pct", 45),
     ("cavity", "tile_rounds", 1), ("channel", "tile_rounds", 0), ("rayleigh_benard", "tile_rounds", 1),
-    ("cavity", "tent_th", 64), ("channel", "lexw_edge_pct", 100), ("backwards_step", "lexw_ramp_pct", 0),
+    ("cavity", "tent_th", 64), ("channel", "lexw_edge_pct", 75), ("backwards_step", "lexw_ramp_pct", 0),
+    ("cavity@4096", "lexw_edge_pct", 100), ("cavity@1024", "lexw_edge_pct", 75),
 ])
 def test_tuning_defaults(case, knob, value):
     """The launch-plan defaults a solver starts with (cfd_tuning_default, host
     only): the measured band floors (16 rows for the channel and every
     reference-order march, 24 for the red-black step and cavity -
-    profiles/r4_tune), boundary-column band lengths, LDS tiles for the
-    cavity only."""
+    profiles/r4_tune), boundary-column band lengths (reference order: 75 %
+    up to 2048 rows, 100 % above), LDS tiles for the cavity only."""
     case, _, order = case.partition("/")
-    cp = C.solver.to_cparams(C.make_params(case), ordering=order or "lex")
+    case, _, n = case.partition("@")
+    cp = C.solver.to_cparams(C.make_params(case, **({"nx": int(n), "ny": int(n)} if n else {})),
+                             ordering=order or "lex")
     v = ctypes.c_int(-1)
     assert _lib.lib().cfd_tuning_default(ctypes.byref(cp), _lib.TUNING[knob], ctypes.byref(v)) == 0
     assert v.value == value
