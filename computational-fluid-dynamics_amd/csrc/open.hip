@@ -436,13 +436,13 @@ __global__ __launch_bounds__(256, CFD_OPEN_MIN_WAVES) void poisson_open_proof_ke
   if (CASE == BACKSTEP && c0 <= c.step_i + 1) gmax = min(gmax, c.inlet_jmax);
   if (!cols_in) open_march<NS, CASE, 1, true, true>(x, y0, y1, dm, pm, gmin, gmax);
   // safe bands alternate their direction (flags bit 0) in the channel only:
-  // the step's launch is faster without the second copy of its loop
-  // (54.9 -> 53.0 us; the channel's 31 -> 35 us without it: profiles/r4_icache)
+  // measured neutral for the step (one copy of its loop: smaller code)
+  // (the channel: 31 -> 35 us without them, profiles/r4_icache)
   else if (CASE == CHANNEL && safe && up) open_march<NS, CASE, -1, false, false>(x, y0, y1, dm, pm);
   else if (safe) open_march<NS, CASE, 1, false, false>(x, y0, y1, dm, pm);
   // (row-checked bands march down only: one copy of that code, which few
-  // waves run, in the instruction cache beside the safe bands' loops - the
-  // channel's launch 32.2 -> 30.6 us, profiles/r4_icache)
+  // waves run, in the instruction cache beside the safe bands' loops; neutral
+  // within noise, profiles/r4_icache)
   else open_march<NS, CASE, 1, false, true>(x, y0, y1, dm, pm, gmin, gmax);
   double growth = 1.0;
 #pragma unroll
