@@ -20,7 +20,7 @@ SEGS = ["load", "red", "red_barrier", "black", "black_barrier", "refresh", "resi
 case, nx, ny = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 400
 cp = C.make_params(case, nx=nx, ny=ny, max_iters=iters)
-s = C.solver_for(cp, device=0)
+s = C.solver_for(cp, device=0, ordering="rb")  # (the tile launches: red-black order)
 s.step()
 s.synchronize()
 t = s.timing()
