@@ -192,6 +192,11 @@ __device__ __forceinline__ double2 lx_ld(const WaveCtx<CAVITY>& x, const double*
 // which split the march loop into dozens of blocks, serialise its loads and
 // ran the ramp launches at half the steady kernel's speed.)
 constexpr int LX_ACT = 1;
+// 1: the open cases' row-checked marches run their groups of 10 steps clear
+// of the ghost rows unchecked (lx_march)
+#ifndef CFD_LEXW_GROUPS
+#define CFD_LEXW_GROUPS 0
+#endif
 constexpr int LX_SAMPLE = 2;  // sampled residual rows (lx_res_row)
 struct LxAct {
   bool a, b, c;    // u, u-1, u-2 within [0, 2(K-1)]
@@ -683,6 +688,29 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
   // (nsteps + 9 <= 127 by the host's band limit: bits t/2 < 64)
 #define LX_BIT(T) ((((st + (T)) >> 1) < 64) ? (1ull << ((st + (T)) >> 1)) : 0ull)
   for (int st = 0; st < nsteps; st += 10, R -= 10) {
+#if CFD_LEXW_GROUPS
+    if constexpr (RC && !EDGE && CASE != CAVITY) {
+      // a group of 10 steps whose updated rows (R-8 .. R+2NS) avoid the ghost
+      // rows, row 1 (its residual reads the bottom ghost's stand-in) and the
+      // stored strip's edge rows runs the unchecked rows (row kinds all
+      // interior: the same operations), as open.hip's marches do; the
+      // row-checked bands otherwise take ~3x a safe band's time per step
+      // (profiles/r4_lexw_stamps)
+      if (R - 8 >= 2 && R - 8 > x.rmin && R + 2 * NS <= x.g.ny && R + 2 * NS < x.rmax) {
+        lx_step<CASE, NS, 0, 0, 0, MODE, EDGE, false>(x, lc, L, cl, s, R, LX_BIT(0));
+        lx_step<CASE, NS, 1, 1, 1, MODE, EDGE, false>(x, lc, L, cl, s, R - 1, LX_BIT(1));
+        lx_step<CASE, NS, 2, 2, 0, MODE, EDGE, false>(x, lc, L, cl, s, R - 2, LX_BIT(2));
+        lx_step<CASE, NS, 3, 3, 1, MODE, EDGE, false>(x, lc, L, cl, s, R - 3, LX_BIT(3));
+        lx_step<CASE, NS, 4, 4, 0, MODE, EDGE, false>(x, lc, L, cl, s, R - 4, LX_BIT(4));
+        lx_step<CASE, NS, 5, 0, 1, MODE, EDGE, false>(x, lc, L, cl, s, R - 5, LX_BIT(5));
+        lx_step<CASE, NS, 6, 1, 0, MODE, EDGE, false>(x, lc, L, cl, s, R - 6, LX_BIT(6));
+        lx_step<CASE, NS, 7, 2, 1, MODE, EDGE, false>(x, lc, L, cl, s, R - 7, LX_BIT(7));
+        lx_step<CASE, NS, 8, 3, 0, MODE, EDGE, false>(x, lc, L, cl, s, R - 8, LX_BIT(8));
+        lx_step<CASE, NS, 9, 4, 1, MODE, EDGE, false>(x, lc, L, cl, s, R - 9, LX_BIT(9));
+        continue;
+      }
+    }
+#endif
     lx_step<CASE, NS, 0, 0, 0, MODE, EDGE, RC>(x, lc, L, cl, s, R, LX_BIT(0));
     lx_step<CASE, NS, 1, 1, 1, MODE, EDGE, RC>(x, lc, L, cl, s, R - 1, LX_BIT(1));
     lx_step<CASE, NS, 2, 2, 0, MODE, EDGE, RC>(x, lc, L, cl, s, R - 2, LX_BIT(2));
@@ -726,6 +754,19 @@ __host__ __device__ inline void lexw_rows(const Geo& g, int H0, int K, int ns, i
     *hi = min(g.wj1, H0 + 2 * ns - 1 - cmin);
   }
 }
+
+// diagnostic build only (CFD_LEXW_STAMPS=1, never the product library): per
+// launch (H0 / 2NS) and march path (0 wall tiles, 1 unmasked, 2 masked, 3
+// steady interior; +4 row-checked open-case variants) the maximum and the
+// sum of the waves' march cycles and the wave count (solver.hip
+// cfd_lexw_stamps, scripts/dbg/lexw_stamps.py)
+#ifndef CFD_LEXW_STAMPS
+#define CFD_LEXW_STAMPS 0
+#endif
+#if CFD_LEXW_STAMPS
+constexpr int LEXW_STAMP_LAUNCHES = 8192;
+static __device__ unsigned long long lexw_stamp_buf[LEXW_STAMP_LAUNCHES * 8 * 3];
+#endif
 
 // One launch of NS lexicographic-order sweeps (half-sweeps H0 .. H0+2NS-1) on
 // one strip, tiled as poisson_multi_kernel (PairPlan). RAMP = false: a launch
@@ -832,17 +873,25 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   const int shard = bl & (LEXW_SHARDS - 1);
   const bool edge = !cols_in;
   constexpr int SM = SAMPLE ? LX_SAMPLE : 0;
+#if CFD_LEXW_STAMPS
+  long long t0_;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0_)::"memory");
+  int path_ = 0;
+#define LX_PATH(v) (path_ = (v))
+#else
+#define LX_PATH(v) ((void)0)
+#endif
   if constexpr (!OPEN) {
     if constexpr (RAMP) {
       // tiles of a ramp launch whose every cell is active in every half-sweep
       // it evaluates (H0-1 .. H0+2NS-1) take the unmasked march
       const bool full = smax <= H0 - 2 && Hend <= smin + last;
-      if (edge) lx_march<CASE, NS, LX_ACT | SM, true>(x, lc, L, y0, y1, c0, lane, shard);
-      else if (full) lx_march<CASE, NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard);
-      else lx_march<CASE, NS, LX_ACT | SM, false>(x, lc, L, y0, y1, c0, lane, shard);
+      if (edge) { LX_PATH(0); lx_march<CASE, NS, LX_ACT | SM, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (full) { LX_PATH(1); lx_march<CASE, NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard); }
+      else { LX_PATH(2); lx_march<CASE, NS, LX_ACT | SM, false>(x, lc, L, y0, y1, c0, lane, shard); }
     } else {
-      if (edge) lx_march<CASE, NS, SM, true>(x, lc, L, y0, y1, c0, lane, shard);
-      else lx_march<CASE, NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard);
+      if (edge) { LX_PATH(0); lx_march<CASE, NS, SM, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else { LX_PATH(3); lx_march<CASE, NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard); }
     }
   } else {
     // row checks unless every row the march updates (y0-H+1 .. y1+H+2NS) lies
@@ -861,16 +910,31 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     const bool edge = edge_;
     if constexpr (RAMP) {
       const bool full = !rc && smax <= H0 - 2 && Hend <= smin + 2 * (K - 1);
-      if (edge) lx_march<CASE, NS, LX_ACT | SM, true, true>(x, lc, L, y0, y1, c0, lane, shard);
-      else if (full) lx_march<CASE, NS, SM, false, false>(x, lc, L, y0, y1, c0, lane, shard);
-      else if (rc) lx_march<CASE, NS, LX_ACT | SM, false, true>(x, lc, L, y0, y1, c0, lane, shard);
-      else lx_march<CASE, NS, LX_ACT | SM, false, false>(x, lc, L, y0, y1, c0, lane, shard);
+      if (edge) { LX_PATH(0); lx_march<CASE, NS, LX_ACT | SM, true, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (full) { LX_PATH(1); lx_march<CASE, NS, SM, false, false>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (rc) { LX_PATH(6); lx_march<CASE, NS, LX_ACT | SM, false, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else { LX_PATH(2); lx_march<CASE, NS, LX_ACT | SM, false, false>(x, lc, L, y0, y1, c0, lane, shard); }
     } else {
-      if (edge) lx_march<CASE, NS, SM, true, true>(x, lc, L, y0, y1, c0, lane, shard);
-      else if (rc) lx_march<CASE, NS, SM, false, true>(x, lc, L, y0, y1, c0, lane, shard);
-      else lx_march<CASE, NS, SM, false, false>(x, lc, L, y0, y1, c0, lane, shard);
+      if (edge) { LX_PATH(0); lx_march<CASE, NS, SM, true, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (rc) { LX_PATH(7); lx_march<CASE, NS, SM, false, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else { LX_PATH(3); lx_march<CASE, NS, SM, false, false>(x, lc, L, y0, y1, c0, lane, shard); }
     }
   }
+#if CFD_LEXW_STAMPS
+  {
+    long long t1_;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_)::"memory");
+    const int li = H0 / (2 * NS);
+    if (lane == 0 && li >= 0 && li < LEXW_STAMP_LAUNCHES) {
+      unsigned long long* b = lexw_stamp_buf + ((size_t)li * 8 + path_) * 3;
+      const unsigned long long cyc = (unsigned long long)(t1_ - t0_);
+      atomicMax(b, cyc);
+      atomicAdd(b + 1, cyc);
+      atomicAdd(b + 2, 1ull);
+    }
+  }
+#endif
+#undef LX_PATH
 }
 
 #undef LX_SLOT

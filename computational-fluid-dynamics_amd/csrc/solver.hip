@@ -1906,6 +1906,17 @@ int cfd_get_field(cfd_solver* s, int field, double* host, size_t count) {
   });
 }
 
+#if CFD_LEXW_STAMPS
+// diagnostic build only: per reference-order launch (H0 / 2NS) and march path,
+// {max, sum of wave cycles, waves} (lexw.hpp lexw_stamp_buf), accumulated since
+// the library loaded
+extern "C" int cfd_lexw_stamps(unsigned long long* out, int n) {
+  if (n > cfd::LEXW_STAMP_LAUNCHES * 8 * 3) n = cfd::LEXW_STAMP_LAUNCHES * 8 * 3;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cfd::lexw_stamp_buf), (size_t)n * 8) == hipSuccess ? n : -1;
+}
+#endif
+
 #if CFD_MARCH_STAMPS
 // diagnostic build only: per wave {tile, column tile, band, y0, y1, interior
 // columns, safe, cycles} of the last poisson_multi_kernel launch
