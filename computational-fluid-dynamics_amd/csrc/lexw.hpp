@@ -192,10 +192,10 @@ __device__ __forceinline__ double2 lx_ld(const WaveCtx<CAVITY>& x, const double*
 // which split the march loop into dozens of blocks, serialise its loads and
 // ran the ramp launches at half the steady kernel's speed.)
 constexpr int LX_ACT = 1;
-// 1: the open cases' row-checked marches run their groups of 10 steps clear
-// of the ghost rows unchecked (lx_march)
+// 1: the channel's row-checked marches run their groups of 10 steps clear of
+// the ghost rows unchecked (lx_march)
 #ifndef CFD_LEXW_GROUPS
-#define CFD_LEXW_GROUPS 0
+#define CFD_LEXW_GROUPS 1
 #endif
 constexpr int LX_SAMPLE = 2;  // sampled residual rows (lx_res_row)
 struct LxAct {
@@ -689,13 +689,15 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
 #define LX_BIT(T) ((((st + (T)) >> 1) < 64) ? (1ull << ((st + (T)) >> 1)) : 0ull)
   for (int st = 0; st < nsteps; st += 10, R -= 10) {
 #if CFD_LEXW_GROUPS
-    if constexpr (RC && !EDGE && CASE != CAVITY) {
+    if constexpr (RC && !EDGE && CASE == CHANNEL) {
       // a group of 10 steps whose updated rows (R-8 .. R+2NS) avoid the ghost
       // rows, row 1 (its residual reads the bottom ghost's stand-in) and the
       // stored strip's edge rows runs the unchecked rows (row kinds all
-      // interior: the same operations), as open.hip's marches do; the
-      // row-checked bands otherwise take ~3x a safe band's time per step
-      // (profiles/r4_lexw_stamps)
+      // interior: the same operations), as open.hip's marches do: the
+      // channel's row-checked bands otherwise take ~3x a safe band's time per
+      // step and set its launch (34.8 -> 30.9 us, 169 -> 181 GLUPS; the
+      // step measured 116.5 -> 114.4 and keeps them checked:
+      // profiles/r4_lexw_stamps)
       if (R - 8 >= 2 && R - 8 > x.rmin && R + 2 * NS <= x.g.ny && R + 2 * NS < x.rmax) {
         lx_step<CASE, NS, 0, 0, 0, MODE, EDGE, false>(x, lc, L, cl, s, R, LX_BIT(0));
         lx_step<CASE, NS, 1, 1, 1, MODE, EDGE, false>(x, lc, L, cl, s, R - 1, LX_BIT(1));
