@@ -75,6 +75,7 @@ __host__ __device__ constexpr int lexw_ch(int ns) { return ns >= 5 ? 10 : 8; }
 constexpr int LEXW_RAMP_BANDS = 256;
 struct LexRamp {
   int nb, th, row0;
+  int wsplit;  // 1: the wall column tiles (first, last) march each band as two half bands (two waves)
   unsigned band[LEXW_RAMP_BANDS];
 };
 
@@ -804,12 +805,28 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     }
     const unsigned e = rp.band[lo];
     const int ca = (e >> 8) & 255, cb = e & 255;
-    ctile = ca + (tile - (int)(e >> 16));
+    int o = tile - (int)(e >> 16), half = -1;
+    // wall tiles (masked march, slower per step; they set the ramp launches'
+    // time): two waves each, one per half band (host: launch_lexw build)
+    if (rp.wsplit && ca == 0 && cb >= ca) {
+      if (o < 2) half = o, o = 0;
+      else o -= 1;
+    }
+    ctile = ca + o;
+    if (half < 0 && rp.wsplit && cb == pl.ctiles - 1 && cb > 0 && ctile >= cb) {
+      half = ctile - cb;
+      ctile = cb;
+    }
     if (ctile > cb) return;
     int rlo, rhi;
     lexw_rows(g, H0, K, NS, ctile, &rlo, &rhi, OPEN);
     y0 = max(rp.row0 + lo * rp.th, rlo);
     y1 = min(rp.row0 + (lo + 1) * rp.th, rhi + 1);
+    if (half >= 0) {
+      const int mid = rp.row0 + lo * rp.th + rp.th / 2;
+      if (half == 0) y1 = min(y1, mid);
+      else y0 = max(y0, mid);
+    }
   } else {
     const int ne = (pl.ctiles >= 2) ? 2 : 1;
     const int nbe = pl.nbe0 + pl.nbe1, nbi = pl.nb0 + pl.nb1;

@@ -24,6 +24,14 @@
 #include "smlex.hpp"
 #include "seqsum.hpp"
 
+// 1: the reference order's ramp launches march the wall column tiles as two
+// half bands each (lexw.hpp LexRamp::wsplit): the wall tiles' masked march set
+// the ramp launches' time (per-launch stamps); cavity 4096^2 704-717 -> 717-729
+// GLUPS, channel and 1024^2 neutral to +0.5 % (profiles/r4_lexw_stamps)
+#ifndef CFD_LEXW_WALL_SPLIT
+#define CFD_LEXW_WALL_SPLIT 1
+#endif
+
 namespace cfd {
 
 static thread_local std::string g_last_error;
@@ -996,6 +1004,7 @@ class Solver {
       }
       if (rh < rl) return;
       const int ex = lexw_extra(ns);
+      rp.wsplit = CFD_LEXW_WALL_SPLIT && P.case_id != CFD_BACKSTEP;  // (the step: -0.5 %, profiles/r4_lexw_stamps)
       auto build = [&](int th) {  // fills rp for band height th; returns the tile count
         rp.th = th;
         rp.row0 = rl;
@@ -1013,6 +1022,10 @@ class Solver {
           rp.band[b] = ((unsigned)n << 16) | ((unsigned)ca << 8) | (unsigned)(cb < 0 ? 0 : cb);
           if (cb < 0) rp.band[b] = ((unsigned)n << 16) | 1u << 8;  // ca 1 > cb 0: empty
           n += std::max(0, cb - ca + 1);
+          if (rp.wsplit && cb >= ca) {  // a second wave per wall tile (lexw.hpp: half bands)
+            if (ca == 0) ++n;
+            if (cb == pl.ctiles - 1 && cb > 0) ++n;
+          }
         }
         return n;
       };
