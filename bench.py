@@ -147,6 +147,10 @@ def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch
     tm = s.timing()
     s.close()
     steady_ms = tm.poisson_steady_ms / max(tm.poisson_steady_launches, 1)
+    ns = round(tm.poisson_sweeps / max(tm.poisson_launches, 1))
+    rows = cells_per_launch // (cp.nx + 2)
+    st_traffic, st_src = pmc_traffic(args.case, "lex", cp.nx, rows - 2, rows, ns,
+                                     sor_template(args.case, _lib_sor_kernel(tm), ns, False))
     achieved = BYTES_PER_CELL * cells_per_launch / (steady_ms * 1e-3) / 1e9 if tm.poisson_steady_launches else None
     return {"ordering": "lex", "value": round(tm.poisson_cell_updates / el / 1e6, 2), "unit": "MLUPS",
             "ms_per_step": round(el / args.lex_steps * 1e3, 3), "steps": args.lex_steps,
@@ -159,22 +163,67 @@ def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch
             "steady_launch_us": round(steady_ms * 1e3, 2) if tm.poisson_steady_launches else None,
             "steady_achieved_GBs": round(achieved, 1) if achieved else None,
             "steady_frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "steady_traffic": pmc_traffic(f"r4_pmc_{args.case}_lex_{cp.nx}x{cells_per_launch // (cp.nx + 2) - 2}.json",
-                                          cp.nx, cells_per_launch // (cp.nx + 2),
-                                          round(tm.poisson_sweeps / max(tm.poisson_launches, 1)))}
+            "steady_traffic": st_traffic, "steady_traffic_source": st_src}
 
 
-def pmc_traffic(name: str, nx: int, rows: int, sweeps: int):
-    """HBM bytes per SOR launch from a committed PMC pass (profiles/, made by
-    scripts/pmc_traffic.sh + pmc_traffic.py on the same workload), or None."""
-    path = os.path.join(ROOT, "profiles", name)
+CASE_ID = {"cavity": 0, "channel": 1, "backwards_step": 2}
+
+
+def sor_template(kcase: str, sor_kernel: str, sweeps: int, proof: bool) -> str | None:
+    """The C++ template instance of the SOR kernel a run's launches went to, as
+    rocprofv3 names it (the PMC files' kernel_match): csrc/march.hpp
+    poisson_multi_kernel<CASE, NS, PROOF>, tile.hip poisson_tile_kernel<CASE,
+    PROOF>, open.hip poisson_open_proof_kernel<CASE, NS>, lexw.hpp
+    poisson_lexw_kernel<CASE, NS, RAMP, SAMPLE> (steady launches of a capped
+    solve: RAMP false, sampled residual rows)."""
+    c = CASE_ID[kcase]
+    if sor_kernel == "lexw":
+        return f"poisson_lexw_kernel<{c}, {sweeps}, false, true>"
+    if sor_kernel == "tile":
+        return f"poisson_tile_kernel<{c}, {'true' if proof else 'false'}>"
+    if sor_kernel == "march":
+        if proof and kcase != "cavity":
+            return f"poisson_open_proof_kernel<{c}, {sweeps}>"
+        if sweeps >= 2:
+            return f"poisson_multi_kernel<{c}, {sweeps}, {'true' if proof else 'false'}>"
+    return None
+
+
+def pmc_traffic(case: str, order: str, nx: int, ny: int, rows: int, sweeps: int, template: str | None):
+    """HBM bytes per SOR launch from the newest committed PMC pass of the same
+    workload (profiles/r<N>_pmc_<case>_<order>_<nx>x<ny>.json, made by
+    scripts/profile_case.sh + pmc_traffic.py), returned only when that file's
+    kernel_match is the kernel instance that ran here (same grid rows and
+    sweeps per launch); otherwise None. Second value: the provenance (file,
+    kernel, commit the profile was taken at) or why there is none."""
+    import glob
+    import re
+
+    pat = os.path.join(ROOT, "profiles", f"r*_pmc_{case}_{order}_{nx}x{ny}.json")
+    found = []
+    for f in glob.glob(pat):
+        m = re.match(r"r(\d+)_pmc_", os.path.basename(f))
+        if m:
+            found.append((int(m.group(1)), f))
+    if not found:
+        return None, {"reason": f"no profiles/r*_pmc_{case}_{order}_{nx}x{ny}.json"}
+    rnd, path = max(found)  # the newest round's pass only (an older one may predate a kernel change)
+    src = {"file": os.path.relpath(path, ROOT)}
     try:
         d = json.load(open(path))
-    except (OSError, ValueError):
-        return None
-    if d.get("nx") == nx and d.get("rows") == rows and d.get("sweeps_per_launch", 1) == sweeps:
-        return d.get("hbm_bytes_per_launch")
-    return None
+    except (OSError, ValueError) as e:
+        return None, dict(src, reason=f"unreadable: {e}")
+    src.update(kernel_match=d.get("kernel_match"), commit=d.get("commit"))
+    if template is None or d.get("kernel_match") != template:
+        return None, dict(src, reason=f"kernel mismatch: profile {d.get('kernel_match')!r}, ran {template!r}")
+    if not (d.get("nx") == nx and d.get("rows") == rows and d.get("sweeps_per_launch", 1) == sweeps):
+        return None, dict(src, reason="grid / sweeps per launch mismatch")
+    return d.get("hbm_bytes_per_launch"), src
+
+
+def _lib_sor_kernel(tm) -> str:
+    from cfd_amd import _lib
+    return _lib.SOR_KERNEL.get(tm.sor_kernel, "?")
 
 
 def kcase_of(case: str) -> str:
@@ -368,15 +417,16 @@ def run(args, rank: int, world: int, local_rank: int, comm, group, loopback: boo
         # the same launch measured as if each sweep streamed its own 24 B/cell
         # (the unfused algorithm's traffic): the temporal-blocking gain
         effective = achieved * sweeps_per_launch
-        # HBM bytes per launch from the committed PMC pass of the same workload (profiles/)
-        traffic = pmc_traffic(f"r4_pmc_{args.case}_{args.ordering}_{cp.nx}x{wrows - 2}.json", cp.nx, wrows,
-                              round(sweeps_per_launch))
         mlups = updates / elapsed / 1e6
         kcase = kcase_of(args.case)
         # red-black launches: proof-mode convergence test (DESIGN.md §2;
         # --proof-test off evaluates the residual in every sweep)
         proof = (args.ordering == "rb" and args.proof_test != "off"
                  and (sor_kernel == "tile" or (sor_kernel == "march" and round(sweeps_per_launch) >= 3)))
+        # HBM bytes per launch from the committed PMC pass of the same workload
+        # and kernel instance (profiles/), with its provenance
+        traffic, traffic_src = pmc_traffic(args.case, args.ordering, cp.nx, wrows - 2, wrows, round(sweeps_per_launch),
+                                           sor_template(kcase, sor_kernel, round(sweeps_per_launch), proof))
         rows_here = g1 - g0 + 1
         per_gpu = (f"{cp.nx}x{rows_here} fp64 cells per GPU (global {cp.nx}x{cp.ny} split over {n_gpus} GPUs)"
                    if strong else f"{cp.nx}x{args.ny} fp64 cells per GPU (global {cp.nx}x{cp.ny})")
@@ -418,6 +468,7 @@ def run(args, rank: int, world: int, local_rank: int, comm, group, loopback: boo
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": (f"poisson_lexw_kernel<{kcase},{round(sweeps_per_launch)},sampled> (steady launches)" if lexw
                            else f"poisson_tile_kernel<{kcase},{'proof' if proof else 'exact'}> "
                                 f"({round(sweeps_per_launch)} sweeps per launch)"

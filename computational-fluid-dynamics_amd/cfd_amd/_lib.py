@@ -106,6 +106,7 @@ SIGNATURES = {
     "cfd_comm_init": (_vp, [ctypes.POINTER(ctypes.c_ubyte), _i, _i, _i]),
     "cfd_comm_destroy": (_i, [_vp]),
     "cfd_comm_info": (_i, [_vp, _ip, _ip, _ip]),
+    "cfd_comm_exchange_check": (_i, [_vp, _i, ctypes.c_size_t, ctypes.POINTER(ctypes.c_longlong)]),
     "cfd_comm_loopback_hub": (_vp, [_i]),
     "cfd_comm_init_loopback": (_vp, [_vp, _i, _i]),
     "cfd_comm_loopback_hub_destroy": (_i, [_vp]),

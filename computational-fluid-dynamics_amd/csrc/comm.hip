@@ -283,6 +283,68 @@ void comm_recv(Comm* c, double* buf, size_t count, int peer, void* stream) {
         "ncclRecv");
 }
 
+// The strip decomposition's halo exchange (Solver::exchange): one group of
+// send / recv pairs, this rank's rows to the rank below (peer_lo) and above
+// (peer_hi) and their rows into this rank's halos; peer < 0: no neighbour.
+// Pairs to one peer match in issue order (the peer's first send to this rank
+// lands in this rank's first receive from it).
+void comm_halo_exchange(Comm* c, const double* send_lo, double* recv_lo, int peer_lo, const double* send_hi,
+                        double* recv_hi, int peer_hi, size_t count, void* stream) {
+  comm_group_start(c);
+  if (peer_lo >= 0) {
+    comm_send(c, send_lo, count, peer_lo, stream);
+    comm_recv(c, recv_lo, count, peer_lo, stream);
+  }
+  if (peer_hi >= 0) {
+    comm_send(c, send_hi, count, peer_hi, stream);
+    comm_recv(c, recv_hi, count, peer_hi, stream);
+  }
+  comm_group_end(c, stream);
+}
+
+// Transport check on device buffers of `count` doubles: both neighbours of the
+// halo exchange are `peer` (the rank itself: RCCL's send / recv to self, which
+// a one-GPU box can run). Send buffers carry a pattern of (rank, side, index);
+// the receives must hold the peer's pattern bit for bit: returns the number of
+// mismatching doubles.
+long long comm_exchange_check(Comm* c, int peer, size_t count) {
+  if (!c) throw Error(CFD_E_ARG, "null communicator");
+  if (peer < 0 || peer >= c->nranks) throw Error(CFD_E_ARG, "peer outside the communicator");
+  if (count == 0) throw Error(CFD_E_ARG, "count must be > 0");
+  LHIP(hipSetDevice(c->device));
+  auto pat = [&](int rank, int side, size_t k) { return (double)rank * 1e9 + side * 1e8 + (double)k + 0.375; };
+  std::vector<double> h(count);
+  double* d[4] = {nullptr, nullptr, nullptr, nullptr};  // send_lo, recv_lo, send_hi, recv_hi
+  hipStream_t st = nullptr;
+  long long bad = 0;
+  try {
+    for (double*& x : d) LHIP(hipMalloc(&x, count * sizeof(double)));
+    LHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    for (int side = 0; side < 2; ++side) {
+      for (size_t k = 0; k < count; ++k) h[k] = pat(c->rank, side, k);
+      LHIP(hipMemcpy(d[2 * side], h.data(), count * sizeof(double), hipMemcpyHostToDevice));
+      LHIP(hipMemset(d[2 * side + 1], 0xff, count * sizeof(double)));  // (NaN until received)
+    }
+    comm_halo_exchange(c, d[0], d[1], peer, d[2], d[3], peer, count, st);
+    LHIP(hipStreamSynchronize(st));
+    for (int side = 0; side < 2; ++side) {
+      LHIP(hipMemcpy(h.data(), d[2 * side + 1], count * sizeof(double), hipMemcpyDeviceToHost));
+      for (size_t k = 0; k < count; ++k) {
+        const double e = pat(peer, side, k);
+        if (std::memcmp(&h[k], &e, sizeof e) != 0) ++bad;
+      }
+    }
+  } catch (...) {
+    for (double* x : d)
+      if (x) (void)hipFree(x);
+    if (st) (void)hipStreamDestroy(st);
+    throw;
+  }
+  for (double* x : d) (void)hipFree(x);
+  (void)hipStreamDestroy(st);
+  return bad;
+}
+
 void comm_allreduce_max(Comm* c, double* buf, size_t count, void* stream) {
   if (c->hub) { loop_allreduce(c, buf, count, 1, static_cast<hipStream_t>(stream)); return; }
   check(rccl().AllReduce(buf, buf, count, ncclFloat64, ncclMax, static_cast<ncclComm_t>(c->nccl),

@@ -48,6 +48,9 @@ void comm_group_start(Comm* c);
 void comm_group_end(Comm* c, void* stream);
 void comm_send(Comm* c, const double* buf, size_t count, int peer, void* stream);
 void comm_recv(Comm* c, double* buf, size_t count, int peer, void* stream);
+void comm_halo_exchange(Comm* c, const double* send_lo, double* recv_lo, int peer_lo, const double* send_hi,
+                        double* recv_hi, int peer_hi, size_t count, void* stream);
+long long comm_exchange_check(Comm* c, int peer, size_t count);
 void comm_allreduce_max(Comm* c, double* buf, size_t count, void* stream);
 void comm_allreduce_sum(Comm* c, double* buf, size_t count, void* stream);
 

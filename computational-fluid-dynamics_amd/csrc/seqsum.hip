@@ -7,21 +7,25 @@
 // rounded before the next term is added, so the sum is one chain of dependent
 // fp64 adds: its time is the add latency times the terms, whatever the
 // parallelism around it. The kernel therefore keeps the chain fed and nothing
-// else on it: one 512-thread workgroup, waves 1-7 stage the terms of the next
-// chunk (SEQ_CHUNK terms in loop order, a solid cell as -0.0, which leaves
-// every sum unchanged: x + -0.0 == x, -0.0 + -0.0 == -0.0, as skipping it
-// does) into LDS while wave 0 adds the current chunk, reading the terms as
-// broadcast LDS loads (every lane the same address) one batch ahead of the
-// adds. One barrier per chunk.
+// else on it: one 256-thread workgroup (one wave per SIMD), waves 1-3 stage
+// the terms of the next chunk (SEQ_CHUNK terms in loop order, a solid cell as
+// -0.0, which leaves every sum unchanged: x + -0.0 == x, -0.0 + -0.0 == -0.0,
+// as skipping it does) into LDS, SEQ_LOADS global loads in flight per thread,
+// while wave 0, alone on its SIMD, adds the current chunk: broadcast LDS loads
+// (every lane the same address) of the next batch are issued before the adds
+// of this one (a compiler barrier keeps them there; otherwise the loads sink
+// to their use and every batch waits for its own LDS round trip). One barrier
+// per chunk.
 #include "seqsum.hpp"
 
 namespace cfd {
 
 namespace {
 
-constexpr int SEQ_THREADS = 512;
-constexpr int SEQ_CHUNK = 4096;  // terms per LDS chunk; two chunks (64 KiB)
-constexpr int SEQ_BATCH = 32;    // terms the adder has in registers, the next batch in flight
+constexpr int SEQ_THREADS = 256;  // wave 0 adds; waves 1-3 stage (one wave per SIMD)
+constexpr int SEQ_CHUNK = 8192;   // terms per LDS chunk; two chunks (128 KiB)
+constexpr int SEQ_BATCH = 32;     // terms the adder has in registers, the next batch in flight
+constexpr int SEQ_LOADS = 8;      // global loads in flight per staging thread
 
 __global__ __launch_bounds__(SEQ_THREADS) void seq_sum_kernel(Geo g, Coef c, const double* __restrict__ a,
                                                               const double* __restrict__ b, int mode,
@@ -32,28 +36,33 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_sum_kernel(Geo g, Coef c, con
   const int nx = g.nx;
   const long long n = (long long)max(0, jb - ja + 1) * nx;  // terms: q -> (ja + q / nx, 1 + q % nx)
   const int nch = (int)((n + SEQ_CHUNK - 1) / SEQ_CHUNK);
-  // waves 1..7: the terms of chunk ch into dst, in loop order
+  // waves 1..3: the terms of chunk ch into dst, in loop order; each thread
+  // issues SEQ_LOADS loads before it writes any of them
   auto produce = [&](int ch, double* dst) {
+    constexpr int STEP = SEQ_THREADS - 64;
     const long long q0 = (long long)ch * SEQ_CHUNK;
-    int e = t - 64;
-    long long q = q0 + e;
-    int jq = (int)(q / nx);
-    int i = 1 + (int)(q - (long long)jq * nx);
-    constexpr int STEP = SEQ_THREADS - 64;  // (448 < nx is not assumed: the row advance loops)
-    for (; e < SEQ_CHUNK; e += STEP) {
-      double tv = -0.0;
-      if (q < n) {
-        const int j = ja + jq;
-        const size_t o = at(g, j, i);
-        const double v = (mode == 0) ? a[o] : 0.5 * (a[o] * a[o] + b[o] * b[o]);
-        tv = is_fluid(c, nx, g.ny, j, i) ? v : -0.0;
+    for (int e0 = t - 64; e0 < SEQ_CHUNK; e0 += STEP * SEQ_LOADS) {
+      double v[SEQ_LOADS];
+      bool ok[SEQ_LOADS];
+#pragma unroll
+      for (int u = 0; u < SEQ_LOADS; ++u) {
+        const int e = e0 + u * STEP;
+        const long long q = q0 + e;
+        ok[u] = e < SEQ_CHUNK && q < n;
+        v[u] = -0.0;
+        if (ok[u]) {
+          const int jq = (int)(q / nx);
+          const int i = 1 + (int)(q - (long long)jq * nx);
+          const int j = ja + jq;
+          const size_t o = at(g, j, i);
+          v[u] = (mode == 0) ? a[o] : 0.5 * (a[o] * a[o] + b[o] * b[o]);
+          ok[u] = is_fluid(c, nx, g.ny, j, i);
+        }
       }
-      dst[e] = tv;
-      q += STEP;
-      i += STEP;
-      while (i > nx) {
-        i -= nx;
-        ++jq;
+#pragma unroll
+      for (int u = 0; u < SEQ_LOADS; ++u) {
+        const int e = e0 + u * STEP;
+        if (e < SEQ_CHUNK) dst[e] = ok[u] ? v[u] : -0.0;
       }
     }
   };
@@ -68,18 +77,27 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_sum_kernel(Geo g, Coef c, con
       // the chunk's tail past n holds -0.0 (no change), so whole batches run
       const double* src = buf[ch & 1];
       const long long left = n - (long long)ch * SEQ_CHUNK;
-      const int len = (int)(left < SEQ_CHUNK ? (left + SEQ_BATCH - 1) / SEQ_BATCH * SEQ_BATCH : SEQ_CHUNK);
+      const int len = (int)(left < SEQ_CHUNK ? (left + 2 * SEQ_BATCH - 1) / (2 * SEQ_BATCH) * (2 * SEQ_BATCH)
+                                             : SEQ_CHUNK);
+      // two register batches in turn (no copies): the loads of one are issued
+      // before the adds of the other; the asm ties the adds to the point after
+      // the loads (they may not be hoisted above them), and the loads may not
+      // sink below it
       double d[SEQ_BATCH], e[SEQ_BATCH];
 #pragma unroll
       for (int u = 0; u < SEQ_BATCH; ++u) d[u] = src[u];
-      for (int k = 0; k < len; k += SEQ_BATCH) {
-        const int kn = (k + SEQ_BATCH < len) ? k + SEQ_BATCH : k;  // (the last batch reloads itself: unused)
+      for (int k = 0; k < len; k += 2 * SEQ_BATCH) {
 #pragma unroll
-        for (int u = 0; u < SEQ_BATCH; ++u) e[u] = src[kn + u];
+        for (int u = 0; u < SEQ_BATCH; ++u) e[u] = src[k + SEQ_BATCH + u];
+        asm volatile("" : "+v"(s)::"memory");
 #pragma unroll
         for (int u = 0; u < SEQ_BATCH; ++u) s += d[u];
+        const int kn = (k + 2 * SEQ_BATCH < len) ? k + 2 * SEQ_BATCH : k;  // (the last pair reloads itself: unused)
 #pragma unroll
-        for (int u = 0; u < SEQ_BATCH; ++u) d[u] = e[u];
+        for (int u = 0; u < SEQ_BATCH; ++u) d[u] = src[kn + u];
+        asm volatile("" : "+v"(s)::"memory");
+#pragma unroll
+        for (int u = 0; u < SEQ_BATCH; ++u) s += e[u];
       }
     }
     __syncthreads();

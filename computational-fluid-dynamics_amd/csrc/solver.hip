@@ -281,7 +281,7 @@ class Solver {
       P.case_id = CFD_CAVITY;
       P.u_ref = 0.0;
     }
-    validate();
+    validate((int)rows.size());
     C = make_coef(P);
     proof_enabled = P.proof_test != CFD_OFF;
     proof_ns = P.sweeps_per_launch == 3 ? 3 : 4;
@@ -307,8 +307,9 @@ class Solver {
       pps = std::max(1, std::min(pps, 4));
       // device-independent plan defaults (params.cpp cfd_tuning_default):
       // cavity boundary-column bands 80 % of the interior march (lane-constant
-      // indicators), the open cases 45 %; band floor 16 rows for the channel,
-      // 24 otherwise; LDS tiles for the cavity only
+      // indicators), the open cases 45 %; band floor 16 rows for the channel
+      // and the reference order, 24 for the red-black cavity / step; LDS tiles
+      // for the cavity only
       for (int knob : {CFD_TUNE_LEXW_EDGE_PCT, CFD_TUNE_PAIR_EDGE_PCT, CFD_TUNE_MARCH_MIN_TH, CFD_TUNE_TENT_TH,
                        CFD_TUNE_LEXW_RAMP_PCT, CFD_TUNE_TILE_ROUNDS, CFD_TUNE_MARCH_ORDER}) {
         int v = 0;
@@ -489,7 +490,7 @@ class Solver {
     st = st_b = nullptr;
   }
 
-  void validate() const {
+  void validate(int nstrips) const {
     if (P.case_id < 0 || P.case_id > 2) throw Error(CFD_E_ARG, "unknown case_id");
     if (P.nx < 2 || P.ny < 2) throw Error(CFD_E_ARG, "grid must have at least 2 interior cells per direction");
     if (!(P.dx > 0) || !(P.dy > 0) || !(P.dt > 0) || !(P.nu > 0) || !(P.rho > 0))
@@ -519,6 +520,11 @@ class Solver {
     if (P.ordering == CFD_ORDER_LEX && P.case_id == CFD_BACKSTEP && !step_lexw_ok() && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
       throw Error(CFD_E_ARG, "lexicographic ordering of a backwards step with a block under 2 cells wide or high "
                              "supports nx + ny < 12000");
+    // (that step runs the one-workgroup kernel, solve_lex: one strip; rejected
+    // here rather than at the first solve)
+    if (P.ordering == CFD_ORDER_LEX && P.case_id == CFD_BACKSTEP && !step_lexw_ok() && nstrips > 1)
+      throw Error(CFD_E_ARG, "lexicographic ordering of a backwards step with a block under 2 cells wide or high "
+                             "runs on one strip (n_strips = 1)");
 #if CFD_WT_STORE
     // (write-through p_out stores address a strip's buffer with 32-bit buffer records)
     if ((double)(P.ny + 2 * HALO + 2) * (double)(((P.nx + 3) + 15) / 16 * 16) * 8.0 >= 4294967295.0)
@@ -555,16 +561,9 @@ class Solver {
       double* base = s.b[b];
       const size_t cnt = (size_t)depth * pitch;
       auto row = [&](int j) { return base + (size_t)(j - g.row_lo) * pitch; };
-      comm_group_start(comm);
-      if (comm->rank > 0) {
-        comm_send(comm, row(g.j0), cnt, comm->rank - 1, xs);
-        comm_recv(comm, row(g.j0 - depth), cnt, comm->rank - 1, xs);
-      }
-      if (comm->rank < comm->nranks - 1) {
-        comm_send(comm, row(g.j1 - depth + 1), cnt, comm->rank + 1, xs);
-        comm_recv(comm, row(g.j1 + 1), cnt, comm->rank + 1, xs);
-      }
-      comm_group_end(comm, xs);
+      comm_halo_exchange(comm, row(g.j0), row(g.j0 - depth), comm->rank > 0 ? comm->rank - 1 : -1,
+                         row(g.j1 - depth + 1), row(g.j1 + 1), comm->rank < comm->nranks - 1 ? comm->rank + 1 : -1,
+                         cnt, xs);
     }
   }
 
@@ -2017,6 +2016,13 @@ int cfd_comm_info(void* comm, int* nranks, int* rank, int* transport) {
   return guard([&] {
     if (!nranks || !rank || !transport) throw Error(CFD_E_ARG, "null output");
     cfd::comm_info(static_cast<cfd::Comm*>(comm), nranks, rank, transport);
+  });
+}
+
+int cfd_comm_exchange_check(void* comm, int peer, size_t count, long long* mismatches) {
+  return guard([&] {
+    if (!mismatches) throw Error(CFD_E_ARG, "null output");
+    *mismatches = cfd::comm_exchange_check(static_cast<cfd::Comm*>(comm), peer, count);
   });
 }
 

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 9
+#define CFD_AMD_ABI_VERSION 10
 
 /* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
  * tree (only figures): it is the cavity's projection step with a resting lid
@@ -214,8 +214,8 @@ enum cfd_tuning {
   CFD_TUNE_LEXW_EDGE_PCT = 3, /* wall-tile band length, % of the interior band (10..100; default 75 up to
                                  2048 rows, 100 above) */
   CFD_TUNE_PAIR_EDGE_PCT = 4, /* boundary-column band length of red-black launches, % (10..100) */
-  CFD_TUNE_MARCH_MIN_TH = 5,  /* minimum rows per band of a march launch (>= 1; default 16 for the channel,
-                                 24 otherwise) */
+  CFD_TUNE_MARCH_MIN_TH = 5,  /* minimum rows per band of a march launch (>= 1; default 16 for the channel
+                                 and for the reference order, 24 for the red-black cavity / step) */
   CFD_TUNE_TENT_TH = 6,       /* rows per band of the predictor's march (>= 4) */
   CFD_TUNE_LEXW_RAMP_PCT = 7, /* lexicographic ramp launches: band height floor, % of the steady plan's (0..100) */
   CFD_TUNE_TILE_ROUNDS = 8,   /* red-black, one strip: LDS-tile launches when the grid fits this many
@@ -244,6 +244,13 @@ int cfd_comm_destroy(void* comm);
 /* What the transport itself reports: for RCCL, ncclCommCount / ncclCommUserRank
  * (so a host can show that RCCL saw every rank); transport 0 = RCCL, 1 = loopback. */
 int cfd_comm_info(void* comm, int* nranks, int* rank, int* transport);
+
+/* Transport check (ABI 10): one halo exchange through the solver's own send / recv group
+ * (comm.hip comm_halo_exchange, as Solver::exchange issues it) with `peer` as both neighbours, on
+ * device buffers of `count` doubles holding a (rank, side, index) pattern; *mismatches = doubles
+ * received that differ from the peer's pattern. peer = the caller's rank exercises RCCL's send /
+ * recv to self, which a one-GPU host can run. */
+int cfd_comm_exchange_check(void* comm, int peer, size_t count, long long* mismatches);
 
 /* In-process transport with the same semantics, for ranks that share one
  * device and run in separate host threads of one process (RCCL refuses two

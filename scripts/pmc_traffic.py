@@ -2,10 +2,13 @@
 """FETCH_SIZE / WRITE_SIZE per SOR launch (scripts/pmc_traffic.sh) -> HBM bytes
 per launch with the gfx950 corrections (FETCH_SIZE x2 for 16-B/lane streaming
 reads, WRITE_SIZE exact for 16-B/lane stores: MI355X_MICROARCH.md, HBM
-[CDNA4]). usage: pmc_traffic.py DIR KERNEL_SUBSTRING OUT.json [NX] [SWEEPS_PER_LAUNCH] [NY]"""
+[CDNA4]). CFD_COMMIT (the git commit of the profiled tree, set by the caller:
+the GPU box has no .git) is recorded as "commit"; bench.py reports it as the
+traffic's provenance. usage: pmc_traffic.py DIR KERNEL_SUBSTRING OUT.json [NX] [SWEEPS_PER_LAUNCH] [NY]"""
 import csv
 import glob
 import json
+import os
 import statistics
 import sys
 
@@ -40,6 +43,7 @@ res = {"kernel_match": ksub, "nx": nx, "ny": ny, "rows": rows, "sweeps_per_launc
                      "(exact for 16-B/lane stores): MI355X_MICROARCH.md, HBM [CDNA4]",
        "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wb, "hbm_bytes_per_launch": rd + wb,
        "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": (rd + wb) / alg,
+       "commit": os.environ.get("CFD_COMMIT") or None,
        "command": f"scripts/pmc_traffic.sh (rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE, separate passes), {d}"}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

@@ -41,6 +41,38 @@ def test_one_rank_rccl_equals_single_domain(case, steps):
         assert all(d["same"].values()), d
 
 
+def test_one_rank_rccl_send_recv_to_self():
+    """ncclSend / ncclRecv on hardware: the halo exchange's own group
+    (comm_halo_exchange) with the one rank as both of its neighbours, on
+    halo-sized device buffers (8 rows of a 4096-column strip), one row and one
+    double; every received double must equal the sent one bit for bit."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29615")
+    out = subprocess.run([sys.executable, "-u", os.path.join(HERE, "rccl_self_exchange.py")],
+                         env=env, capture_output=True, text=True, timeout=100)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["comm"] == {"nranks": 1, "rank": 0, "transport": "rccl"}
+    assert "error" not in d, d
+    assert d["mismatches"] == {"32896": 0, "4112": 0, "1": 0}, d
+
+
+def test_loopback_exchange_check():
+    """The same check through the loopback transport (one rank, peer = itself)."""
+    import ctypes
+
+    from cfd_amd import _lib
+    L = _lib.lib()
+    hub = L.cfd_comm_loopback_hub(1)
+    comm = L.cfd_comm_init_loopback(hub, 0, 0)
+    assert comm, L.cfd_last_error()
+    bad = ctypes.c_longlong(-1)
+    assert L.cfd_comm_exchange_check(comm, 0, 4112, ctypes.byref(bad)) == 0, L.cfd_last_error()
+    assert bad.value == 0
+    assert L.cfd_comm_exchange_check(comm, 1, 16, ctypes.byref(bad)) != 0  # (peer outside the communicator)
+    L.cfd_comm_destroy(comm)
+    L.cfd_comm_loopback_hub_destroy(hub)
+
+
 def _gpu_count() -> int:
     try:
         import torch

@@ -130,9 +130,58 @@ def test_smlex_equals_multiblock_march(case, steps):
         assert bits_equal(a.field(f), b.field(f)), f
 
 
+# grids past 4096 cells: more than 2 cells per thread and colour (MAXC 4: up to
+# 8192 cells, MAXC 5: up to 10240), the cells' own values read from LDS
+# (!PCREG), the source in LDS (FLDS), the cavity's multipliers rebuilt at every
+# update (smlex.hip poisson_smlex_kernel)
+MAXC_GRIDS = [("cavity", 70, 70, 4), ("channel", 120, 40, 4), ("backwards_step", 100, 60, 4),
+              ("cavity", 96, 96, 5), ("channel", 110, 80, 5), ("backwards_step", 128, 72, 5)]
+
+
+def maxc_of(nx, ny):  # smlex.hip smlex_launch
+    per_colour = (nx * ny + 1) // 2
+    return 2 if per_colour <= 2 * 1024 else 4 if per_colour <= 4 * 1024 else 5
+
+
+@pytest.mark.parametrize("case,nx,ny,maxc", MAXC_GRIDS)
+def test_maxc_variants_bitexact(case, nx, ny, maxc):
+    """Whole timesteps on grids that take the MAXC 4 / 5 kernels: bit for bit
+    the oracle's reference loop, one launch per solve."""
+    assert maxc_of(nx, ny) == maxc
+    steps = 2 if case == "backwards_step" else 4
+    cp = C.make_params(case, nx=nx, ny=ny)
+    g, _ = run_pair(cp, steps)
+    assert _lib.SOR_KERNEL[g.timing().sor_kernel] == "smlex"
+    assert g.timing().poisson_launches == steps
+
+
+@pytest.mark.parametrize("case,nx,ny,maxc", MAXC_GRIDS)
+def test_maxc_variants_caps_around_checkpoints_bitexact(case, nx, ny, maxc):
+    """Capped solves around the checkpoint interval on the MAXC 4 / 5 grids
+    (the last iteration's refresh duties and the checkpoint replay there)."""
+    M = interval(C.make_params(case, nx=nx, ny=ny))
+    for cap in (1, 2, M - 1, M, M + 1, 2 * M + 1):
+        cp = C.make_params(case, nx=nx, ny=ny, max_iters=cap)
+        g, its = run_pair(cp, 2)
+        assert all(i <= cap for i in its)
+        assert _lib.SOR_KERNEL[g.timing().sor_kernel] == "smlex"
+
+
+@pytest.mark.parametrize("nx,ny,kernel", [(110, 88, "smlex"), (140, 69, "lexw")])
+def test_lds_limit_boundary(nx, ny, kernel):
+    """smlex_fits past 4096 cells: p and the source both in LDS, 2 (nx+2)(ny+2)
+    <= SMLEX_CELLS = 20160. (nx+2)(ny+2) = 10080 fits, 10082 does not; the
+    grid that does not fit runs the multi-block march, bit for bit the same."""
+    assert (nx + 2) * (ny + 2) == (10080 if kernel == "smlex" else 10082)
+    cp = C.make_params("cavity", nx=nx, ny=ny)
+    g, _ = run_pair(cp, 2)
+    assert _lib.SOR_KERNEL[g.timing().sor_kernel] == kernel
+
+
 def test_large_grid_keeps_multiblock_march():
-    """Past the LDS (p and its previous values: (nx+2)(ny+2) <= 10048) the
-    reference order runs the multi-block march."""
+    """Past the LDS (grids over 4096 cells: p and the source in LDS,
+    2 (nx+2)(ny+2) <= SMLEX_CELLS = 20160; up to 4096 cells: (nx+2)(ny+2) <=
+    20160) the reference order runs the multi-block march."""
     g = C.solver_for(C.make_params("cavity", nx=128, ny=128), ordering="lex")
     g.applyBoundaryConditions()
     g.step()

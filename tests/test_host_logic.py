@@ -44,7 +44,7 @@ def test_nm_exports_match_header():
 
 
 def test_abi_version():
-    assert _lib.lib().cfd_abi_version() == 9
+    assert _lib.lib().cfd_abi_version() == 10
 
 
 def test_params_struct_layout_matches_header(tmp_path):
@@ -231,6 +231,23 @@ def test_tuning_defaults(case, knob, value):
     assert b"occupancy" in _lib.lib().cfd_last_error()
 
 
+def test_thin_step_lex_on_strips_rejected_at_create():
+    """A backwards step whose block is under 2 cells wide or high runs the
+    reference order on the one-workgroup kernel (one strip): with more strips
+    cfd_create rejects it before any device is touched, not the first solve."""
+    p = C.make_params("backwards_step", nx=64, ny=32)
+    p.h_inlet = 1.9375  # inlet_jmax = 31 = ny - 1: the block is one cell high
+    cp = C.solver.to_cparams(p)
+    assert cp.inlet_jmax == p.ny - 1
+    assert cp.ordering == _lib.ORDER["lex"]
+    h = _lib.lib().cfd_create(ctypes.byref(cp), 0, 2)
+    assert not h
+    assert b"one strip" in _lib.lib().cfd_last_error()
+    cp.ordering = _lib.ORDER["rb"]  # red-black takes any block on strips (fails here only for want of a GPU)
+    h = _lib.lib().cfd_create(ctypes.byref(cp), 0, 2)
+    assert b"one strip" not in _lib.lib().cfd_last_error()
+
+
 def test_bad_switch_rejected_before_device():
     cp = C.solver.to_cparams(C.make_params("cavity"))
     cp.overlap = 7
@@ -275,3 +292,33 @@ def test_host_binaries_built_and_print_usage():
         assert os.access(exe, os.X_OK), exe
         r = subprocess.run([exe, "--help"], capture_output=True, text=True)
         assert r.returncode == 0 and "--Re" in r.stderr and "--Nx" in r.stderr and "--dt" in r.stderr
+
+
+def test_bench_traffic_provenance(tmp_path, monkeypatch):
+    """bench.py reports roofline.traffic from the newest committed PMC pass of
+    the same workload only when that pass profiled the kernel instance that
+    ran (its kernel_match), with the file and commit as traffic_source; a
+    mismatched kernel, grid or sweep count gives traffic null."""
+    import json as _json
+
+    import bench
+
+    assert bench.sor_template("cavity", "march", 4, True) == "poisson_multi_kernel<0, 4, true>"
+    assert bench.sor_template("channel", "march", 4, True) == "poisson_open_proof_kernel<1, 4>"
+    assert bench.sor_template("cavity", "tile", 4, True) == "poisson_tile_kernel<0, true>"
+    assert bench.sor_template("backwards_step", "lexw", 4, False) == "poisson_lexw_kernel<2, 4, false, true>"
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    rec = {"kernel_match": "poisson_multi_kernel<0, 4, true>", "nx": 64, "rows": 66, "sweeps_per_launch": 4,
+           "hbm_bytes_per_launch": 123.0, "commit": "abc123"}
+    (prof / "r4_pmc_cavity_rb_64x64.json").write_text(_json.dumps(dict(rec, hbm_bytes_per_launch=99.0)))
+    (prof / "r5_pmc_cavity_rb_64x64.json").write_text(_json.dumps(rec))
+    t, src = bench.pmc_traffic("cavity", "rb", 64, 64, 66, 4, "poisson_multi_kernel<0, 4, true>")
+    assert t == 123.0 and src["file"].endswith("r5_pmc_cavity_rb_64x64.json") and src["commit"] == "abc123"
+    t, src = bench.pmc_traffic("cavity", "rb", 64, 64, 66, 4, "poisson_multi_kernel<0, 3, true>")
+    assert t is None and "kernel mismatch" in src["reason"]  # (the older r4 file is not a fallback)
+    t, src = bench.pmc_traffic("cavity", "rb", 64, 64, 66, 3, "poisson_multi_kernel<0, 4, true>")
+    assert t is None and "mismatch" in src["reason"]
+    t, src = bench.pmc_traffic("channel", "rb", 64, 64, 66, 4, "poisson_open_proof_kernel<1, 4>")
+    assert t is None and "no profiles" in src["reason"]
