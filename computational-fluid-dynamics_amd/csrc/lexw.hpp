@@ -167,6 +167,14 @@ struct LexCtx {
   double tol;
   double o2, o3, o4;  // omega / nc (Coef::om_nc) held as values: a select of
                       // Coef fields becomes a select of addresses and a load
+  // open cases (lxo_row): the row refreshed as a copy of the row below it,
+  // at its own skew time (the top ghost row ny + 1; in the step's column
+  // tiles left of its column, the block's bottom row: the rows above it never
+  // change), the last row with residuals, and what the copy adds to the value
+  // (-0.0: an exact copy, the ghost rule; +0.0: the step's solid refresh
+  // 0.0 + p_S, backwards_step-01.cpp:708-738, which turns -0.0 into +0.0)
+  int jg, jr1;
+  double gz;
 };
 
 // Row R of a field at this lane's column pair, row and column clamped to
@@ -197,6 +205,12 @@ constexpr int LX_ACT = 1;
 // the ghost rows unchecked (lx_march)
 #ifndef CFD_LEXW_GROUPS
 #define CFD_LEXW_GROUPS 1
+#endif
+// A/B build only: every interior band of the open cases on the row-checked
+// march (one interior code path in the kernel: is the checked path slow for
+// its work or for the instruction cache it shares with the safe path?)
+#ifndef CFD_LEXW_ALLRC
+#define CFD_LEXW_ALLRC 0
 #endif
 constexpr int LX_SAMPLE = 2;  // sampled residual rows (lx_res_row)
 struct LxAct {
@@ -375,7 +389,7 @@ __device__ __forceinline__ int lxs_class(const WaveCtx<CAVITY>& x, int i) {
 
 template <int CASE, bool EDGE, bool RC, bool STEP>
 __device__ __forceinline__ double lxo_value(const WaveCtx<CAVITY>& x, int rk, int ck, int rs, int cs, double pc,
-                                            double pW, double pE, double pS, double pN, double fc) {
+                                            double pW, double pE, double pS, double pN, double fc, double gz) {
   const double sor = sor_update<CASE>(x.c, 0, 0, 0, 0, pc, pW, pE, pS, pN, fc);
   if constexpr (!RC && !EDGE) return sor;
   double nv = sor;
@@ -384,8 +398,8 @@ __device__ __forceinline__ double lxo_value(const WaveCtx<CAVITY>& x, int rk, in
     nv = (rs == 0 || cs == 2) ? sor : solid;
   }
   if constexpr (EDGE) nv = (ck == 3) ? nv : (ck == 1) ? pE : (ck == 2) ? 0.0 : pc;
-  if constexpr (RC) {  // row kinds: 1 bottom ghost (copy N), 2 top ghost (copy S), 3 keep
-    const double g = (rk == 1) ? pN : pS;
+  if constexpr (RC) {  // row kinds: 1 bottom ghost (copy N), 2 top ghost (copy S + gz), 3 keep
+    const double g = (rk == 1) ? pN : pS + gz;
     if (EDGE) nv = (rk == 0) ? nv : (rk != 3 && ck == 3) ? g : pc;
     else nv = (rk == 0) ? nv : (rk != 3) ? g : pc;
   }
@@ -404,8 +418,10 @@ __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& 
   double2& mn = W[LX_SLOT(X + 1)];
   const double2 nb = mn, sb = W[LX_SLOT(X - 1)];  // rows j+1 (N), j-1 (S)
   const double2 old = m;
-  // row kind (row-uniform): 0 interior, 1 bottom ghost, 2 top ghost, 3 keep (halo edge / outside)
-  const int rk = !RC ? 0 : (j == 0) ? 1 : (j == x.g.ny + 1) ? 2 : (j > x.rmin && j < x.rmax) ? 0 : 3;
+  // row kind (row-uniform): 0 interior, 1 bottom ghost, 2 top ghost (or the
+  // step's bottom solid row in a left tile: LexCtx::jg), 3 keep (halo edge /
+  // outside; the rows above jg)
+  const int rk = !RC ? 0 : (j == 0) ? 1 : (j == lc.jg) ? 2 : (j > x.rmin && j < x.rmax) ? 0 : 3;
   const int jb = x.c.inlet_jmax + 1;
   const int rs = !STEP ? 0 : (j < jb) ? 0 : (j == jb) ? 1 : 2;  // (row-uniform)
   const bool rowc = STEP && j == jb - 1 && rk == 0;              // the corner's south neighbour's row
@@ -419,7 +435,7 @@ __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& 
     const double cv = ((0.0 + nb.y) + m.x) * 0.5;  // E = (jb, si+1) is slot b of this lane in row jb
     const double pN = (isc && !first) ? cv : nb.x;
     const double nv = lxo_value<CASE, EDGE, RC, STEP>(x, rk, cc.ka, rs, cc.sa, m.x, dpp_from_left(m.y), m.y, sb.x,
-                                                      pN, fc.x);
+                                                      pN, fc.x, lc.gz);
     bool on = true;
     if constexpr ((MODE & LX_ACT) != 0) {
       // left / bottom ghost and step-column solid: two half-sweeps later. (The
@@ -470,7 +486,7 @@ __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& 
     const double cv = ((0.0 + dpp_from_right(nb.x)) + m.y) * 0.5;  // E = slot a of lane + 1 in row jb
     const double pN = (isc && !first) ? cv : nb.y;
     const double nv = lxo_value<CASE, EDGE, RC, STEP>(x, rk, cc.kb, rs, cc.sb, m.y, m.x, dpp_from_right(m.x), sb.y,
-                                                      pN, fc.y);
+                                                      pN, fc.y, lc.gz);
     bool on = true;
     if constexpr ((MODE & LX_ACT) != 0) {
       const bool shifted = (RC && rk == 1) || (STEP && rk == 0 && rs == 2 && cc.sb == 1);
@@ -514,7 +530,7 @@ __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& 
     __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
   }
   if constexpr (!RES) return;
-  const bool rrow = j >= x.y0 && j < x.y1 && j >= x.g.j0 && j <= x.g.j1;  // row-uniform
+  const bool rrow = j >= x.y0 && j < x.y1 && j >= x.g.j0 && j <= lc.jr1;  // row-uniform
   const double thr = rrow ? lc.tol : __builtin_huge_val();
   const bool row1 = RC && j == 1;  // S is the bottom ghost: the cell's own value stands in
   bool ex;
@@ -699,7 +715,7 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
       // step and set its launch (34.8 -> 30.9 us, 169 -> 181 GLUPS; the
       // step measured 116.5 -> 114.4 and keeps them checked:
       // profiles/r4_lexw_stamps)
-      if (R - 8 >= 2 && R - 8 > x.rmin && R + 2 * NS <= x.g.ny && R + 2 * NS < x.rmax) {
+      if (R - 8 >= 2 && R - 8 > x.rmin && R + 2 * NS < lc.jg && R + 2 * NS < x.rmax) {
         lx_step<CASE, NS, 0, 0, 0, MODE, EDGE, false>(x, lc, L, cl, s, R, LX_BIT(0));
         lx_step<CASE, NS, 1, 1, 1, MODE, EDGE, false>(x, lc, L, cl, s, R - 1, LX_BIT(1));
         lx_step<CASE, NS, 2, 2, 0, MODE, EDGE, false>(x, lc, L, cl, s, R - 2, LX_BIT(2));
@@ -760,7 +776,8 @@ __host__ __device__ inline void lexw_rows(const Geo& g, int H0, int K, int ns, i
 
 // diagnostic build only (CFD_LEXW_STAMPS=1, never the product library): per
 // launch (H0 / 2NS) and march path (0 wall tiles, 1 unmasked, 2 masked, 3
-// steady interior; +4 row-checked open-case variants) the maximum and the
+// steady interior, 4 the step's block-crossing tiles on the masked march, 5
+// the step's left tiles, 6 / 7 row-checked open-case ramp / steady) the maximum and the
 // sum of the waves' march cycles and the wave count (solver.hip
 // cfd_lexw_stamps, scripts/dbg/lexw_stamps.py)
 #ifndef CFD_LEXW_STAMPS
@@ -852,6 +869,21 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   constexpr int TWC = lexw_twc(NS);
   const int c0 = ctile * TWC - CH;
   const int gi = c0 + 2 * lane;
+  // backwards step: a column tile whose march columns all lie left of the
+  // step's column (the first wall tile included) sees the block's rows jb ..
+  // ny as row-uniform rules: its bottom row jb refreshed as 0.0 + p_S, the
+  // rows above it interior solids that never change, and their ghosts (the
+  // top ghost row, the left ghost column above jb) constants the host set
+  // before the solve (Solver::lexw_presolid). Its bands end at row jb: the
+  // left tiles march as a channel whose top ghost row is jb (lxo_row,
+  // LexCtx::jg), with no per-cell solid rules.
+  bool left = false;
+  if constexpr (CASE == BACKSTEP) {
+    if (c0 + 127 <= c.step_i - 1 && (flags & 8)) {  // (flags bit 3: the host set those ghosts)
+      left = c0 >= 1;
+      y1 = min(y1, c.inlet_jmax + 2);
+    }
+  }
   if (y0 >= y1) return;
 
   // activity of the marched region (rows y0-H-1 .. y1+H, columns c0 .. c0+127,
@@ -888,7 +920,9 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
                             __builtin_amdgcn_readfirstlane(__double2loint(v)));
   };
-  LexCtx lc{H0, K, L.tol[0], uni(c.om_nc[2]), uni(c.om_nc[3]), uni(c.om_nc[4])};
+  LexCtx lc{H0, K, L.tol[0], uni(c.om_nc[2]), uni(c.om_nc[3]), uni(c.om_nc[4]),
+            left ? c.inlet_jmax + 1 : g.ny + 1, left ? min(g.j1, c.inlet_jmax) : g.j1, left ? 0.0 : -0.0};
+  if (left) x.rmax = min(x.rmax, c.inlet_jmax + 2);  // (rows above jb: kept; loads clamped there)
   const int shard = bl & (LEXW_SHARDS - 1);
   const bool edge = !cols_in;
   constexpr int SM = SAMPLE ? LX_SAMPLE : 0;
@@ -915,9 +949,9 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   } else {
     // row checks unless every row the march updates (y0-H+1 .. y1+H+2NS) lies
     // strictly between the stored strip's edge rows (ghost rows included)
-    bool rc = !(y0 - H + 1 > x.rmin && y1 + H + 2 * NS < x.rmax);
+    bool rc = CFD_LEXW_ALLRC || !(y0 - H + 1 > x.rmin && y1 + H + 2 * NS < min(x.rmax, lc.jg));
     bool edge_ = edge;
-    if constexpr (CASE == BACKSTEP) {
+    if (CASE == BACKSTEP && !left) {
       const int jb = c.inlet_jmax + 1, si = c.step_i;
       // a march over interior solids only (rows y0-H-1 .. y1+H+2NS+1 in jb+1 ..
       // ny, columns in 1 .. si-1): nothing it touches ever changes
@@ -944,6 +978,8 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     long long t1_;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_)::"memory");
     const int li = H0 / (2 * NS);
+    if (OPEN && path_ == 0 && cols_in) path_ = 4;  // the step's block / crossing tiles on the masked march
+    if (left) path_ = 5;                           // the step's left tiles
     if (lane == 0 && li >= 0 && li < LEXW_STAMP_LAUNCHES) {
       unsigned long long* b = lexw_stamp_buf + ((size_t)li * 8 + path_) * 3;
       const unsigned long long cyc = (unsigned long long)(t1_ - t0_);
@@ -994,6 +1030,24 @@ __global__ void step_corner_kernel(Geo g, Coef c, double* __restrict__ p) {
   const int jb = c.inlet_jmax + 1, si = c.step_i;
   if (threadIdx.x != 0 || blockIdx.x != 0 || jb < g.j0 || jb > g.j1) return;
   p[at(g, jb, si)] = ((0.0 + p[at(g, jb, si + 1)]) + p[at(g, jb - 1, si)]) * 0.5;
+}
+
+// backwards step, reference order: the ghosts next to the block's interior
+// solids - the top ghost row over columns 1 .. si-1 and the left ghost column
+// over rows jb+1 .. ny - take the values the reference's first refresh after
+// a sweep gives them (backwards_step-01.cpp:688-705: copies of interior
+// solids, which never change) before the solve, in both buffers. Nothing
+// reads them before that refresh (solids are never updated, residuals cover
+// fluid cells only), so the solve's iterates are unchanged, and the march's
+// column tiles left of the step's column end at the block's bottom row
+// (poisson_lexw_kernel, flags bit 3). Owned rows of the strip; halos follow by
+// exchange.
+__global__ void step_presolid_kernel(Geo g, Coef c, double* __restrict__ p) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ny = g.ny, si = c.step_i, jb = c.inlet_jmax + 1;
+  if (t >= 1 && t <= si - 1 && g.wj1 == ny + 1) p[at(g, ny + 1, t)] = p[at(g, ny, t)];
+  const int j = jb + 1 + t;
+  if (j <= ny && j >= g.j0 && j <= g.j1) p[at(g, j, 0)] = p[at(g, j, 1)];
 }
 
 // max-norm residual of an open-case field over its fluid cells

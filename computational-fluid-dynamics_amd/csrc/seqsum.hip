@@ -14,8 +14,10 @@
 // while wave 0, alone on its SIMD, adds the current chunk: broadcast LDS loads
 // (every lane the same address) of the next batch are issued before the adds
 // of this one (a compiler barrier keeps them there; otherwise the loads sink
-// to their use and every batch waits for its own LDS round trip). One barrier
-// per chunk.
+// to their use and every batch waits for its own LDS round trip), in fully
+// unrolled blocks (no register copies). One barrier per chunk. The dependent
+// v_add_f64 chain itself takes 2.9 ns per add on MI355X (tools/add_chain.hip,
+// profiles/r5/add_chain.json).
 #include "seqsum.hpp"
 
 namespace cfd {
@@ -25,6 +27,8 @@ namespace {
 constexpr int SEQ_THREADS = 256;  // wave 0 adds; waves 1-3 stage (one wave per SIMD)
 constexpr int SEQ_CHUNK = 8192;   // terms per LDS chunk; two chunks (128 KiB)
 constexpr int SEQ_BATCH = 32;     // terms the adder has in registers, the next batch in flight
+constexpr int SEQ_BLOCK = 1024;   // terms per unrolled block of the adder (a multiple of SEQ_BATCH)
+static_assert(SEQ_CHUNK % SEQ_BLOCK == 0 && SEQ_BLOCK % SEQ_BATCH == 0, "seqsum blocking");
 constexpr int SEQ_LOADS = 8;      // global loads in flight per staging thread
 
 __global__ __launch_bounds__(SEQ_THREADS) void seq_sum_kernel(Geo g, Coef c, const double* __restrict__ a,
@@ -77,27 +81,26 @@ __global__ __launch_bounds__(SEQ_THREADS) void seq_sum_kernel(Geo g, Coef c, con
       // the chunk's tail past n holds -0.0 (no change), so whole batches run
       const double* src = buf[ch & 1];
       const long long left = n - (long long)ch * SEQ_CHUNK;
-      const int len = (int)(left < SEQ_CHUNK ? (left + 2 * SEQ_BATCH - 1) / (2 * SEQ_BATCH) * (2 * SEQ_BATCH)
-                                             : SEQ_CHUNK);
-      // two register batches in turn (no copies): the loads of one are issued
-      // before the adds of the other; the asm ties the adds to the point after
-      // the loads (they may not be hoisted above them), and the loads may not
-      // sink below it
-      double d[SEQ_BATCH], e[SEQ_BATCH];
+      const int len = (int)(left < SEQ_CHUNK ? (left + SEQ_BLOCK - 1) / SEQ_BLOCK * SEQ_BLOCK : SEQ_CHUNK);
+      // blocks of SEQ_BLOCK terms, each fully unrolled: batch b+1's loads are
+      // issued before batch b's adds (the asm ties the adds to the point after
+      // the loads, and the loads may not sink below it), and the two register
+      // batches alternate by name - no loop-carried copies, which a rolled
+      // loop's registers cost (v_mov per term)
+      for (int k0 = 0; k0 < len; k0 += SEQ_BLOCK) {
+        double d[2][SEQ_BATCH];
 #pragma unroll
-      for (int u = 0; u < SEQ_BATCH; ++u) d[u] = src[u];
-      for (int k = 0; k < len; k += 2 * SEQ_BATCH) {
+        for (int u = 0; u < SEQ_BATCH; ++u) d[0][u] = src[k0 + u];
 #pragma unroll
-        for (int u = 0; u < SEQ_BATCH; ++u) e[u] = src[k + SEQ_BATCH + u];
-        asm volatile("" : "+v"(s)::"memory");
+        for (int bb = 0; bb < SEQ_BLOCK / SEQ_BATCH; ++bb) {
+          if (bb + 1 < SEQ_BLOCK / SEQ_BATCH) {
 #pragma unroll
-        for (int u = 0; u < SEQ_BATCH; ++u) s += d[u];
-        const int kn = (k + 2 * SEQ_BATCH < len) ? k + 2 * SEQ_BATCH : k;  // (the last pair reloads itself: unused)
+            for (int u = 0; u < SEQ_BATCH; ++u) d[(bb + 1) & 1][u] = src[k0 + (bb + 1) * SEQ_BATCH + u];
+          }
+          asm volatile("" : "+v"(s)::"memory");
 #pragma unroll
-        for (int u = 0; u < SEQ_BATCH; ++u) d[u] = src[kn + u];
-        asm volatile("" : "+v"(s)::"memory");
-#pragma unroll
-        for (int u = 0; u < SEQ_BATCH; ++u) s += e[u];
+          for (int u = 0; u < SEQ_BATCH; ++u) s += d[bb & 1][u];
+        }
       }
     }
     __syncthreads();

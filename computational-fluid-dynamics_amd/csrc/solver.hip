@@ -225,6 +225,7 @@ class Solver {
       case CFD_TUNE_LEXW_RAMP_PCT: lexw_ramp_pct = std::max(0, std::min(100, v)); break;
       case CFD_TUNE_TILE_ROUNDS: tile_rounds = std::max(0, std::min(v, 16)); break;
       case CFD_TUNE_MARCH_ORDER: march_flags = (march_flags & ~8) | (v ? 8 : 0); break;
+      case CFD_TUNE_LEXW_LEFT: lexw_left = v != 0; break;
       default: throw Error(CFD_E_ARG, "unknown tuning knob");
     }
   }
@@ -239,6 +240,7 @@ class Solver {
   int resident_lexw_waves = 2048;
   int lexw_edge_pct = 100;  // wall-tile band length, % of the interior band (cfd_tuning_default: 75 up to 2048 rows)
   int lexw_ramp_pct = 0;    // ramp launches: bands at least this % of the steady plan's (CFD_TUNE_LEXW_RAMP_PCT)
+  bool lexw_left = true;    // backwards step: the left column tiles' class (CFD_TUNE_LEXW_LEFT)
   // the multi-block reference-order march (lexw.hpp): cavity (1-4 sweeps per
   // launch), channel and backwards step (4; 3 on strips). The step's solid
   // rules need a block of at least 2 columns and 2 rows (si >= 2, jb <= ny-1);
@@ -311,7 +313,7 @@ class Solver {
       // and the reference order, 24 for the red-black cavity / step; LDS tiles
       // for the cavity only
       for (int knob : {CFD_TUNE_LEXW_EDGE_PCT, CFD_TUNE_PAIR_EDGE_PCT, CFD_TUNE_MARCH_MIN_TH, CFD_TUNE_TENT_TH,
-                       CFD_TUNE_LEXW_RAMP_PCT, CFD_TUNE_TILE_ROUNDS, CFD_TUNE_MARCH_ORDER}) {
+                       CFD_TUNE_LEXW_RAMP_PCT, CFD_TUNE_TILE_ROUNDS, CFD_TUNE_MARCH_ORDER, CFD_TUNE_LEXW_LEFT}) {
         int v = 0;
         if (cfd_tuning_default(&P, knob, &v) == CFD_OK) set_tuning_value(knob, v);
       }
@@ -979,10 +981,25 @@ class Solver {
 
   // steady: every cell active in every half-sweep of the launch and in the
   // previous launch's last one (no activity masks: the leaner kernel)
+  // backwards step, reference order: the block's ghost constants set before
+  // the march (lexw.hpp step_presolid_kernel), so that the column tiles left
+  // of the step's column end at the block's bottom row and march as a channel
+  // below it (flags bit 3; CFD_TUNE_LEXW_LEFT 0: the per-cell masked march)
+  bool lexw_left_class() const { return P.case_id == CFD_BACKSTEP && lexw_left; }
+  void lexw_presolid() {
+    if (!lexw_left_class()) return;
+    for (auto& s : S)
+      for (int b : {0, 1}) {
+        const int n = std::max(C.step_i, P.ny) + 1;
+        step_presolid_kernel<<<(n + 255) / 256, 256, 0, st>>>(s.g, C, s.b[pbuf(b)]);
+        check_launch("step_presolid");
+      }
+  }
+
   void launch_lexw(int ns, bool steady, bool sample, const PairPlan& pl, const Geo& g, const double* pin,
                    double* pout, const double* f, const LexCtl& L, int H0, int K, int ka, int kb, bool replay,
                    int waves) {
-    const int fl = replay ? 4 : 0;
+    const int fl = (replay ? 4 : 0) | (lexw_left_class() ? 8 : 0);
     const int ne = pl.ctiles >= 2 ? 2 : 1;
     int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
     LexRamp rp{};
@@ -1101,6 +1118,7 @@ class Solver {
     const int ms0 = (P.nx + P.ny - 1 + 2 * ns - 1) / (2 * ns), ms1 = floordiv(2 * K - 2 * ns - 1, 2 * ns);
     const bool steady = time_steady && ms1 >= ms0;
     const int chunk = P.chunk > 0 ? P.chunk : 32;
+    if (K >= 1) lexw_presolid();  // (both buffers hold the solve's input here)
     int tested = tests ? ka0 - 1 : K;  // highest iteration tested
     bool stopped = false;
     int m = 0, c = 0;

@@ -221,8 +221,11 @@ enum cfd_tuning {
   CFD_TUNE_TILE_ROUNDS = 8,   /* red-black, one strip: LDS-tile launches when the grid fits this many
                                  resident rounds of tiles (one per CU; 0: never, the march launches;
                                  default 1 for the cavity, 0 for the open cases) */
-  CFD_TUNE_MARCH_ORDER = 9    /* red-black march launches: 0 = the column tiles of a band on consecutive waves
+  CFD_TUNE_MARCH_ORDER = 9,   /* red-black march launches: 0 = the column tiles of a band on consecutive waves
                                  (default), 1 = the bands of a column tile (ABI 9) */
+  CFD_TUNE_LEXW_LEFT = 10     /* reference-order backwards step: 1 = the column tiles left of the step's column end
+                                 at the block's bottom row and march as a channel below it (default), 0 = the
+                                 per-cell masked march over every row that reaches the block (ABI 10) */
 };
 int cfd_set_tuning(cfd_solver* s, int knob, int value);
 /* The default a solver created from these parameters starts with (host only, no

@@ -4,7 +4,7 @@ every launch (H0 / 2NS) and march path the slowest wave's cycles, the mean and
 the wave count; printed as a summary over the ramp-up, steady and ramp-down
 launches.
 
-usage: CFD_AMD_LIB=libcfd_amd_lstamps.so python3 scripts/dbg/lexw_stamps.py case nx ny [max_iters]
+usage: CFD_AMD_LIB=libcfd_amd_lstamps.so python3 scripts/dbg/lexw_stamps.py case nx ny [max_iters] [knob=value ...]
 """
 import ctypes
 import json
@@ -16,11 +16,12 @@ import numpy as np  # noqa: E402
 import cfd_amd as C  # noqa: E402
 from cfd_amd import _lib  # noqa: E402
 
-PATHS = ["wall", "ramp_full", "ramp_masked", "steady", "-", "-", "ramp_masked_rc", "steady_rc"]
+PATHS = ["wall", "ramp_full", "ramp_masked", "steady", "step_block", "step_left", "ramp_masked_rc", "steady_rc"]
 case, nx, ny = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 10000
-cp = C.make_params(case, nx=nx, ny=ny, max_iters=iters)
-s = C.solver_for(cp, device=0, ordering="lex")
+tuning = {k: int(v) for k, v in (a.split("=") for a in sys.argv[5:])}
+cp = C.make_params(case, nx=nx, ny=ny, max_iters=iters, **({"re": 400.0} if case == "backwards_step" else {}))
+s = C.solver_for(cp, device=0, ordering="lex", tuning=tuning)
 s.step()
 s.synchronize()
 L = _lib.lib()

@@ -368,3 +368,75 @@ def test_step_8192x512_step_bitexact_capped():
     assert g.step() == o.step()
     for name in ("u", "v", "p"):
         assert_bits(g.field(name), ofield(o, name, cp), f"step 8192x512 {name}")
+
+
+# ---- the step's column tiles left of its column (lexw.hpp left class) ----
+
+@pytest.mark.parametrize("nx,ny,K,strips", [
+    (1024, 64, 37, 1),   # step_i 256: one left tile (110-column tiles, c0 + 127 <= step_i - 1), the wall tile clipped
+    (1024, 64, 1, 1), (1024, 66, 2, 1),
+    (960, 34, 113, 1),   # jb 18: the edge zone spans most of the left tiles' rows
+    (2000, 40, 23, 1),   # step_i 500: three left tiles
+    (1100, 48, 29, 2), (1300, 40, 41, 3),  # strips (3 sweeps per launch, 112-column tiles)
+])
+def test_step_left_tiles_capped_bitexact(nx, ny, K, strips):
+    """Capped solves with column tiles wholly left of the step's column: they
+    end at the block's bottom row (refreshed as 0.0 + p_S in the skew) and the
+    ghosts over the block's interior take their first-refresh values before
+    the solve (step_presolid_kernel). Random initial fields: every solid and
+    ghost starts off its refreshed value, so a ghost the solve did not set
+    would show."""
+    cp = C.make_params("backwards_step", nx=nx, ny=ny, max_iters=K)
+    assert cp.step_i >= 230
+    f = random_field(cp, 25, 10.0)
+    p0 = random_field(cp, 26)
+    g, o, ((rg, ro),) = solve_step(cp, f, p0, strips)
+    assert rg[0] == ro[0] == K
+    assert rg == ro
+    assert_bits(g.field("p"), o.field("p"), f"step left tiles {nx}x{ny} K={K} strips={strips}")
+
+
+def test_step_left_class_equals_masked_march():
+    """CFD_TUNE_LEXW_LEFT 1 (default) and 0 (every march reaching the block on
+    the per-cell masked path): the same whole timesteps, bit for bit, and the
+    oracle's."""
+    cp = C.make_params("backwards_step", re=400.0, nx=1536, ny=96, max_iters=1000)  # (> (nx+ny)/2: steady launches)
+    out = []
+    for left in (1, 0):
+        g = C.BackwardsStepSolver(cp, ordering="lex", small_solve="off", tuning={"lexw_left": left})
+        its = [g.step() for _ in range(2)]
+        out.append((its, {n: g.field(n) for n in ("u", "v", "p")}))
+        assert g.timing().poisson_steady_launches > 0
+        g.close()
+    assert out[0][0] == out[1][0]
+    for n in ("u", "v", "p"):
+        assert_bits(out[0][1][n], out[1][1][n], f"left class vs masked {n}")
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.velocity_bc(False)
+    assert [o.step() for _ in range(2)] == out[0][0]
+    for n in ("u", "v", "p"):
+        assert_bits(out[0][1][n], ofield(o, n, cp), f"left class vs oracle {n}")
+
+
+def test_step_left_tiles_converging_bitexact():
+    """Converging solves (early stop, replay from the initial field, the
+    open-iteration continuation) with left tiles: the presolid ghosts must
+    not leak into a solve that stops at iteration 0 either."""
+    cp = C.make_params("backwards_step", nx=1024, ny=32, max_iters=5000)
+    cp.tol_factor = 3e-3
+    jb, si = cp.inlet_jmax + 1, cp.step_i
+    f = np.zeros((cp.ny + 2, cp.nx + 2))
+    f[jb - 1, si] = 40.0
+    f[3, 100] = -25.0
+    f[jb - 2, si - 50] = 7.0
+    p0 = random_field(cp, 31, 1e-3)
+    g, o, res = solve_step(cp, f, p0, solves=2)
+    for k, (rg, ro) in enumerate(res):
+        assert rg == ro, k
+    assert_bits(g.field("p"), o.field("p"), "step left tiles converged p")
+    # a solve with no sweep (max_iters 0; the reference's loop always sweeps
+    # once otherwise): the field, ghosts included, stays as given
+    cp0 = C.make_params("backwards_step", nx=1024, ny=32, max_iters=0)
+    g0, o0, ((rg, ro),) = solve_step(cp0, f, p0)
+    assert rg == ro and rg[0] == 0
+    assert_bits(g0.field("p"), o0.field("p"), "iteration-0 stop")
