@@ -1,0 +1,507 @@
+// resident.hip — the register-resident red-black SOR solve (resident.hpp has
+// the design). Own translation unit: device.hpp only.
+#include <algorithm>
+#include <type_traits>
+
+#include "resident.hpp"
+
+namespace cfd {
+
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr unsigned long long RES_SPIN_TICKS = 200000000ull;  // 2 s of the 100 MHz wall clock: a wait that long is a bug
+
+// write-through (sc1) 16-B load / store of a column pair (MI355X_MICROARCH.md
+// "Valid forms", first row: every store of a handed-off byte sc1 and drained
+// before the flag, every load of it sc1)
+__device__ __forceinline__ double2 ld_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16));
+}
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, double2 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v), r, (int)off, 0, 16);
+}
+__device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Lane constants of the two columns a lane holds (slot a: gx, slot b: gx + 1)
+struct ResLane {
+  double om_a, om_b;    // omega / nc of the column below the top row (nc = 4 - walls among W, E), 0 at
+                        // ghost / outside columns
+  double omt_a, omt_b;  // the same in the top row (its north neighbour is the lid's ghost: nc one less)
+  double omm_a, omm_b;  // 1 - omega; 1 at ghost / outside columns
+  double pa, pb;        // 1.0: a proving cell (owned, 1 < i < nx) of a wave whose rows all prove, else 0.0
+};
+
+// sor_update<CAVITY> (cavity-01.cpp:643-654) as pc * omm + om * sum in every
+// cell. The solve's field starts at zero with +0.0 ghosts that never change,
+// so a wall's indicator product 0 * p_ghost is +0.0 = p_ghost itself and only
+// omega / nc differs at the walls (lexw.hpp lx_upd: the same argument); these
+// are per-lane constants, so every wave runs one straight-line update. A
+// ghost / outside column takes om = 0, omm = 1: pc * 1 + 0 * sum = pc for
+// finite sum and pc != -0.0 (the ghosts are +0.0). Region edge lanes 0 / 63
+// and region rows past the halo are updated from zeros: halo, stale anyway
+// (they never reach an owned cell within a group; their SOR stays bounded).
+// f * h^2 is precomputed (the same rounding).
+//
+// One half-sweep of colour COL over a wave's RPW rows, in place (a cell's
+// neighbours are the other colour). Region row parity = q parity (the plan
+// keeps region row 0 on an even grid row), so slot a has colour q & 1. Staged
+// over the rows: every stage is independent across rows (RPW chains in
+// flight). GEN: a wave holding a ghost row (0, ny + 1), the top row (ny) or
+// rows outside the grid - per-row fix-ups (fzm: frozen rows keep their value;
+// tpm: the top row's omega / nc), no proofs. Plain waves (every row in 1 ..
+// ny - 1) record max |p' - p| of their proving black cells (lane multipliers).
+template <int RPW, int COL, bool GEN>
+__device__ __forceinline__ void res_half(const ResLane& L, double2 (&p)[RPW], const double2 (&fh)[RPW],
+                                         const double2& Sx, const double2& Nx, unsigned fzm, unsigned tpm,
+                                         double& dmx) {
+  double pc[RPW], pw[RPW], pe[RPW], sum[RPW], ns[RPW], nv[RPW];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    if ((q & 1) == COL) {
+      pc[q] = p[q].x;
+      pw[q] = dpp_from_left(p[q].y);
+      pe[q] = p[q].y;
+    } else {
+      pc[q] = p[q].y;
+      pw[q] = p[q].x;
+      pe[q] = dpp_from_right(p[q].x);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) sum[q] = pe[q] + pw[q];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const double2 S = (q == 0) ? Sx : p[q - 1];
+    const double2 N = (q == RPW - 1) ? Nx : p[q + 1];
+    ns[q] = ((q & 1) == COL) ? (N.x + S.x) : (N.y + S.y);
+  }
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) sum[q] = sum[q] + ns[q];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) sum[q] = sum[q] - (((q & 1) == COL) ? fh[q].x : fh[q].y);
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const bool A = (q & 1) == COL;
+    nv[q] = pc[q] * (A ? L.omm_a : L.omm_b) + (A ? L.om_a : L.om_b) * sum[q];
+  }
+  if constexpr (GEN) {
+    asm volatile("" : "+s"(fzm), "+s"(tpm));
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const bool A = (q & 1) == COL;
+      if ((tpm >> q) & 1u) nv[q] = pc[q] * (A ? L.omm_a : L.omm_b) + (A ? L.omt_a : L.omt_b) * sum[q];
+      if ((fzm >> q) & 1u) nv[q] = pc[q];
+    }
+  } else if constexpr (COL == 1) {
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) dmx = fmax(dmx, fabs(nv[q] - pc[q]) * (((q & 1) == COL) ? L.pa : L.pb));
+  }
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    if ((q & 1) == COL) p[q].x = nv[q];
+    else p[q].y = nv[q];
+  }
+}
+
+// bounded spin: true = gave up (the wait exceeded RES_SPIN_TICKS)
+__device__ __forceinline__ bool res_spin_expired(unsigned long long t0) {
+  __builtin_amdgcn_s_sleep(1);
+  return wall_clock64() - t0 > RES_SPIN_TICKS;
+}
+
+}  // namespace
+
+// diagnostic build only (CFD_RES_STAMPS=1, never the product library): each
+// wave sums the shader-clock cycles of its group phases over the solve - 0
+// neighbour wait, 1 halo loads, 2 first exchange + proofs, 3 sweeps, 4 group
+// end (bands, drain, flag) - and counts its groups (5); read back by
+// cfd_res_stamps ([tile][wave][6], scripts/dbg/res_stamps.py)
+#ifndef CFD_RES_STAMPS
+#define CFD_RES_STAMPS 0
+#endif
+#if CFD_RES_STAMPS
+constexpr int RES_STAMP_SEGS = 6;
+__device__ unsigned long long res_stamp_buf[256 * RES_MAXW * RES_STAMP_SEGS];
+#define RES_STAMP(seg)                                                          \
+  do {                                                                          \
+    unsigned long long t_;                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                          \
+    st_acc[seg] += t_ - st_last;                                                \
+    st_last = t_;                                                               \
+  } while (0)
+#else
+#define RES_STAMP(seg) ((void)0)
+#endif
+
+// One launch = the whole solve (or its replay to a known count: RES_REPLAY).
+template <int RPW>
+__global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo g, Coef c, const double* __restrict__ pin,
+                                                                             double* __restrict__ pout,
+                                                                             const double* __restrict__ f, ResCtl R,
+                                                                             ResPlan rp, int flags) {
+  constexpr int NS = RES_NS, H = RES_HALO, TW = RES_TW;
+  __shared__ double2 E[2][RES_MAXW][2][64];  // the waves' first / last rows after each half-sweep (by parity)
+  __shared__ double red[RES_MAXW][NS + 1];   // per wave: max |p' - p| per sweep, max |p| of the group's input
+  __shared__ int dec;                         // 0 go on, 1 exit (fallback / stop), 2 exit (timeout)
+  __shared__ int gdec;                        // the group a fallback starts at
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NW = rp.waves;
+  const bool replay = (flags & RES_REPLAY) != 0;
+  if (threadIdx.x == 0) dec = 0;  // (read after the first barrier)
+
+  // tiles of one XCD next to each other (speed only: blocks b and b + 8 share one)
+  const int nblk = (int)gridDim.x;
+  const int L8 = (nblk / 8) * 8;
+  const int bl = (int)blockIdx.x;
+  const int tile = bl < L8 ? (bl % 8) * (nblk / 8) + bl / 8 : bl;
+  const int ntiles = rp.ctiles * rp.rtiles;
+  const int ct = tile % rp.ctiles, rt = tile / rp.ctiles;
+  const int nx = g.nx, ny = g.ny;
+  const int x0 = ct * TW, x1 = min(x0 + TW, nx + 2);  // owned columns [x0, x1)
+  const int y0 = rp.lo + rt * rp.th, y1 = min(y0 + rp.th, rp.hi);  // owned rows [y0, y1)
+  const int gy0 = y0 - H;                    // grid row of region row 0 (even)
+  const int RR = (y1 - y0) + 2 * H;          // region rows (<= NW * RPW: host plan)
+  const int gx = x0 - H + 2 * lane;          // this lane's columns gx, gx + 1 (gx even)
+  const int jb = gy0 + w * RPW;              // grid row of this wave's row 0
+  const int rlo = g.row_lo, rhi = g.row_lo + g.nrows - 1;  // stored rows
+  const int gxc = min(max(gx, 0), g.pitch - 2);
+  const unsigned P = (unsigned)g.pitch;
+  auto offs = [&](int j) { return ((unsigned)(j - rlo) * P + (unsigned)gxc) * 8u; };
+
+  // row classes of this wave (wave-uniform): owned rows, halo rows read at each
+  // group start, frozen rows (ghost rows, rows outside the grid), the top row
+  unsigned ownm = 0, haloh = 0, fzm = 0, tpm = 0, rowm = 0;
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int r = w * RPW + q, j = jb + q;
+    const bool own = j >= y0 && j < y1;
+    if (own) ownm |= 1u << q;
+    if (r < RR) rowm |= 1u << q;  // region rows (the rest: past the halo, never loaded)
+    // region rows read from the neighbours at each group start (grid rows only)
+    if (r < RR && !own && j >= 0 && j <= ny + 1) haloh |= 1u << q;
+    if (j <= 0 || j >= ny + 1) fzm |= 1u << q;
+    if (j == ny) tpm |= 1u << q;
+  }
+  ownm = __builtin_amdgcn_readfirstlane(ownm);
+  haloh = __builtin_amdgcn_readfirstlane(haloh);
+  fzm = __builtin_amdgcn_readfirstlane(fzm);
+  tpm = __builtin_amdgcn_readfirstlane(tpm);
+  rowm = __builtin_amdgcn_readfirstlane(rowm);
+  const bool gen = (fzm | tpm) != 0u;                       // (wave-uniform) the fix-up path
+  const bool proves = !gen && ownm == (1u << RPW) - 1u;     // every row owned and in 1 .. ny - 1
+  // lane constants
+  const bool own_pair = gx >= x0 && gx < x1;
+  ResLane L;
+  {
+    const double o2 = c.om_nc[2], o3 = c.om_nc[3], o4 = c.om_nc[4], omw = c.one_m_omega;
+    auto col = [&](int i, double& om, double& omt, double& omm, double& pr) {
+      const bool in = i >= 1 && i <= nx, wall = i == 1 || i == nx;
+      om = !in ? 0.0 : wall ? o3 : o4;
+      omt = !in ? 0.0 : wall ? o2 : o3;
+      omm = in ? omw : 1.0;
+      pr = (proves && own_pair && i >= 2 && i <= nx - 1) ? 1.0 : 0.0;
+    };
+    col(gx, L.om_a, L.omt_a, L.omm_a, L.pa);
+    col(gx + 1, L.om_b, L.omt_b, L.omm_b, L.pb);
+  }
+  const bool col_in = gx >= 0 && gx <= nx + 1;      // a grid column pair (its halo cells are published)
+  const bool halo_lane = col_in && !own_pair;       // owned rows: this lane's pair belongs to a neighbour
+  const bool band_lane = own_pair && (gx < x0 + H || gx >= x1 - H);  // owned pair in the left / right band
+
+  // the region from p_in (rows / columns clamped to stored memory: clamped
+  // cells lie outside the grid, are never updated and never stored), the
+  // source as f * h^2
+  double2 p[RPW], fh[RPW];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int jc = min(max(jb + q, rlo), rhi);
+    const size_t o = (size_t)(jc - rlo) * (size_t)g.pitch + (size_t)gxc;
+    p[q] = *reinterpret_cast<const double2*>(pin + o);
+    const double2 F = *reinterpret_cast<const double2*>(f + o);
+    fh[q] = make_double2(F.x * c.h2, F.y * c.h2);
+  }
+  const double tol = R.tol[0];
+  // the reference's loop tests the initial residual first (cavity-01.cpp:633)
+  if (!replay && !(R.tol[1] > tol)) {
+    if (tile == 0 && threadIdx.x == 0) {
+      R.status[0] = 1;
+      R.status[1] = 0;
+    }
+    return;
+  }
+  const double fmx = R.tol[2];
+  const int K = R.K, G = res_groups(K);
+  const __amdgpu_buffer_rsrc_t xr[2] = {
+      __builtin_amdgcn_make_buffer_rsrc(R.xa, 0, (int)((unsigned)g.nrows * P * 8u), 0x00020000),
+      __builtin_amdgcn_make_buffer_rsrc(R.xb, 0, (int)((unsigned)g.nrows * P * 8u), 0x00020000)};
+  // Completion spreads one tile per group: when this wave starts group m, its
+  // neighbours' waves have finished group m - 1, theirs m - 2, ..., so every
+  // tile has finished group m - DIAM (DIAM: the tile grid's Chebyshev
+  // diameter). A tile's wave 0 publishes the proofs of group x during group
+  // x + 1 (drained before its flag x + 2), so at the start of group m the
+  // proofs of every group up to m - DIAM - 1 are published: group
+  // m - DIAM - 1 is checked then, with no counter and no grid barrier.
+  const int DIAM = max(rp.ctiles, rp.rtiles) - 1;
+  unsigned* const myflag = R.flags + (size_t)tile * RES_MAXW + w;
+  // the (tile, wave) flags this wave waits for: lane 8n + v = wave v of neighbour n (3x3 ring, centre skipped)
+  int nflag = -1;
+  {
+    const int n = lane >> 3, v = lane & 7, n9 = n < 4 ? n : n + 1;
+    const int tr = rt + n9 / 3 - 1, tc = ct + n9 % 3 - 1;
+    if (v < NW && tr >= 0 && tr < rp.rtiles && tc >= 0 && tc < rp.ctiles) nflag = (tr * rp.ctiles + tc) * RES_MAXW + v;
+  }
+  auto wait_nb = [&](unsigned e) -> bool {  // false: gave up
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      const bool ok = nflag < 0 || ld_flag(R.flags + nflag) >= e;
+      if (__all(ok)) return true;
+      if (res_spin_expired(t0)) return false;
+    }
+  };
+  // proofs of group gq (wave 0): lanes < nsw store "iteration gq*NS + 1 + lane goes on"
+  auto publish_proofs = [&](int gq) {
+    const int nq = min(NS, K - gq * NS);
+    double dm = 0.0, pv = 0.0;
+    if (lane < NS + 1)
+      for (int v = 0; v < NW; ++v) {
+        const double x = red[v][lane];
+        if (lane < NS) dm = fmax(dm, x);
+        else pv = fmax(pv, x);
+      }
+    pv = __shfl(pv, NS, 64);
+    double growth = 1.0;
+    for (int q = 0; q < nq; ++q) growth *= 9.0;
+    const double ratio = proof_ratio_gen(c, tol, dm, pv, fmx, growth);
+    if (lane < nq && ratio > 1.0)
+      __hip_atomic_store(R.proven + gq * NS + 1 + lane, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // the reference's while condition for the tested iterations of group gc
+  // (every one but the cap, which the loop never tests): lane-wise loads
+  auto check_load = [&](int gc) -> bool {
+    const int kk = gc * NS + 1 + lane;
+    const bool tested = lane < NS && kk <= K - 1 && kk % R.check_every == 0;
+    return !tested || ld_flag(R.proven + kk) != 0u;
+  };
+
+#if CFD_RES_STAMPS
+  unsigned long long st_acc[RES_STAMP_SEGS] = {}, st_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
+  int gfail = -1;  // first group left open (fallback)
+  bool pend = true;
+  int pend_g = -1;  // (wave 0) the group whose proofs were loaded at this group's start
+  for (int gi = 0; gi < G; ++gi) {
+    const int nsw = min(NS, K - gi * NS);
+    // ---- group start: the neighbours' edge bands of group gi - 1 (each wave waits for its own)
+    if (gi > 0) {
+      const bool ok = wait_nb((unsigned)gi);
+      RES_STAMP(0);
+      if (!ok) {
+        dec = 2;
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (the loads stay after the poll)
+        const __amdgpu_buffer_rsrc_t xp = xr[(gi - 1) & 1];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+          const bool hrow = (haloh >> q) & 1u;
+          const bool orow = (ownm >> q) & 1u;
+          if ((hrow && col_in) || (orow && halo_lane)) p[q] = ld_sc1(xp, offs(jb + q));
+        }
+      }
+    }
+    pend_g = -1;
+    if (w == 0 && !replay && gi - DIAM - 1 >= 0) {  // evaluated at this group's end
+      pend_g = gi - DIAM - 1;
+      pend = check_load(pend_g);
+    }
+    // max |p| over the region: the proof's P of this group's sweeps
+    double pm = 0.0;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q)
+      if ((rowm >> q) & 1u) pm = fmax(pm, fmax(fabs(p[q].x), fabs(p[q].y)));
+#if CFD_RES_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the halo loads' latency in phase 1)
+#endif
+    RES_STAMP(1);
+    // ---- NS sweeps (red, black), the waves' edge rows through LDS after each half-sweep
+    double2 Sx = make_double2(0.0, 0.0), Nx = Sx;
+    double dmx[NS];
+    int par = 0;
+    auto exchange = [&]() {
+      E[par][w][0][lane] = p[0];
+      E[par][w][1][lane] = p[RPW - 1];
+      __syncthreads();
+      if (w > 0) Sx = E[par][w - 1][1][lane];
+      if (w < NW - 1) Nx = E[par][w + 1][0][lane];
+      par ^= 1;
+    };
+    exchange();
+    // decisions taken at the previous group's end (a timeout now), visible after the barrier
+    if (dec == 2) {
+      if (threadIdx.x == 0) __hip_atomic_store(R.status + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (dec == 1) {
+      gfail = gdec;
+      break;
+    }
+    if (w == 0 && !replay && gi > 0) publish_proofs(gi - 1);  // (red[] of group gi - 1: written before the barrier)
+    RES_STAMP(2);
+    auto sweeps = [&](auto gen_c) {
+      constexpr bool GEN = decltype(gen_c)::value;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        dmx[s] = 0.0;
+        if (s < nsw) {
+          res_half<RPW, 0, GEN>(L, p, fh, Sx, Nx, fzm, tpm, dmx[s]);
+          exchange();
+          res_half<RPW, 1, GEN>(L, p, fh, Sx, Nx, fzm, tpm, dmx[s]);
+          if (s + 1 < nsw) exchange();
+        }
+      }
+    };
+    if (gen) sweeps(std::true_type{});
+    else sweeps(std::false_type{});
+    RES_STAMP(3);
+    // ---- group end: this wave's proof values, its part of the edge bands, its flag
+    if (!replay) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) dmx[s] = wave_max(dmx[s]);
+      pm = wave_max(pm);
+      if (lane == 0) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) red[w][s] = dmx[s];
+        red[w][NS] = pm;
+      }
+    }
+    {
+      const __amdgpu_buffer_rsrc_t xo = xr[gi & 1];
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const int j = jb + q;
+        const bool orow = (ownm >> q) & 1u;
+        const bool brow = j < y0 + H || j >= y1 - H;  // (row-uniform) in the bottom / top band
+        if (orow && own_pair && (brow || band_lane)) st_sc1(xo, offs(j), p[q]);
+      }
+    }
+    if (pend_g >= 0 && !__all(pend) && lane == 0) {  // (wave 0) group pend_g left an iteration open
+      gdec = pend_g;
+      dec = 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the bands (and wave 0's proofs) drained before the flag
+    if (lane == 0) __hip_atomic_store(myflag, (unsigned)(gi + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    RES_STAMP(4);
+#if CFD_RES_STAMPS
+    st_acc[5] += 1;
+#endif
+  }
+#if CFD_RES_STAMPS
+  if (lane < RES_STAMP_SEGS && tile < 256) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int q = 0; q < RES_STAMP_SEGS; ++q) v = lane == q ? st_acc[q] : v;
+    res_stamp_buf[((size_t)tile * RES_MAXW + w) * RES_STAMP_SEGS + lane] = v;
+  }
+#endif
+  if (gfail < 0 && !replay) {
+    // the groups the loop did not check: every tile's last proofs published
+    // (wave 0's flag G + 1), then groups max(0, G - DIAM - 1) .. G - 1 in order
+    __syncthreads();  // (red[] of the last group; dec of the last check)
+    if (dec == 1) {
+      gfail = gdec;
+    } else if (w == 0) {
+      int d = 0;
+      publish_proofs(G - 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(myflag, (unsigned)(G + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long t0 = wall_clock64();
+      for (int t0i = 0; t0i < ntiles && d == 0; t0i += 64) {
+        const int t = t0i + lane;
+        for (;;) {
+          const bool ok = t >= ntiles || ld_flag(R.flags + (size_t)t * RES_MAXW) >= (unsigned)(G + 1);
+          if (__all(ok)) break;
+          if (res_spin_expired(t0)) {
+            d = 2;
+            break;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int gc = max(0, G - DIAM - 1); gc < G && d == 0; ++gc)
+        if (!__all(check_load(gc))) {
+          d = 1;
+          if (lane == 0) gdec = gc;
+        }
+      if (lane == 0) dec = d;
+    }
+    __syncthreads();
+    if (dec == 1) gfail = gdec;
+    if (dec == 2) {
+      if (threadIdx.x == 0) __hip_atomic_store(R.status + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
+  if (gfail >= 0) {  // the host replays to gfail * NS and evaluates from there
+    if (tile == 0 && threadIdx.x == 0) {
+      R.status[0] = 2;
+      R.status[1] = gfail * NS;
+    }
+    return;
+  }
+  // the final field: owned cells -> p_out
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int j = jb + q;
+    if (((ownm >> q) & 1u) && own_pair)
+      *reinterpret_cast<double2*>(pout + (size_t)(j - rlo) * (size_t)g.pitch + (size_t)gx) = p[q];
+  }
+  if (!replay && tile == 0 && threadIdx.x == 0) {
+    R.status[0] = 0;
+    R.status[1] = K;
+  }
+}
+
+#if CFD_RES_STAMPS
+extern "C" int cfd_res_stamps(unsigned long long* out, int n) {
+  const int cap = 256 * RES_MAXW * RES_STAMP_SEGS;
+  if (n > cap) n = cap;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(res_stamp_buf), (size_t)n * 8) == hipSuccess ? n : -1;
+}
+#endif
+
+ResPlan res_plan(int nx, int lo, int hi, int max_tiles) {
+  ResPlan rp{};
+  rp.lo = lo;
+  rp.hi = hi;
+  if ((lo & 1) != 0 || hi <= lo) return ResPlan{};
+  rp.ctiles = (nx + 2 + RES_TW - 1) / RES_TW;
+  const int rows = hi - lo;
+  if (rp.ctiles > max_tiles) return ResPlan{};
+  const int rt = std::max(1, max_tiles / rp.ctiles);
+  rp.th = (rows + rt - 1) / rt;
+  rp.th = std::max(RES_HALO, (rp.th + 1) / 2 * 2);  // even (region row parity), at least one halo deep
+  rp.rtiles = (rows + rp.th - 1) / rp.th;
+  const int rr = rp.th + 2 * RES_HALO;
+  rp.rpw = rr <= 8 * RES_MAXW ? 8 : 0;  // (16 rows per wave spill: not planned)
+  if (rp.rpw == 0) return ResPlan{};  // a tile's region exceeds the register budget
+  rp.waves = (rr + rp.rpw - 1) / rp.rpw;
+  return rp;
+}
+
+void res_launch(int case_id, const Geo& g, const Coef& c, const double* pin, double* pout, const double* f,
+                const ResCtl& R, const ResPlan& rp, int flags, hipStream_t st) {
+  const int n = rp.ctiles * rp.rtiles;
+  if (n <= 0 || case_id != CAVITY) return;
+  const dim3 grid(n), block(rp.waves * 64);
+  if (rp.rpw != 8) return;
+  poisson_resident_kernel<8><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
+}
+
+}  // namespace cfd

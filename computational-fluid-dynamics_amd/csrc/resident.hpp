@@ -1,0 +1,92 @@
+// resident.hpp — the red-black SOR solve as ONE persistent launch whose
+// workgroups keep their tile of p (and the source) in registers for the whole
+// solve: grids of up to a few million cells (BASELINE configs[1] 1024^2,
+// configs[2] 4096x512).
+//
+// Why: at these sizes the per-launch designs are bound by fill, not by HBM.
+// The wave march gives each band 8-16 rows against a 15-19-row pipeline; the
+// LDS tiles (tile.hip) reload and store their tile every 4 sweeps and run
+// their sweeps latency- and barrier-bound out of LDS. Here the
+// whole grid lives in the register files of the 256 CUs (1024^2: 8 KB of p
+// and f per wave, ~30 of 128 VGPRs): nothing moves through HBM between
+// sweeps except the tiles' edge bands.
+//
+// Layout: one workgroup per tile (at most one per CU, all co-resident: a grid
+// of <= CUs workgroups of up to 16 waves and 65 KB of LDS). A tile owns
+// RES_TW = 112 columns x th rows (ghost rows / columns included at the grid's
+// edges) and holds a region of 128 columns x (th + 2 RES_HALO) rows: lane l of
+// every wave holds the column pair (c0 + 2l, c0 + 2l + 1), wave w the region
+// rows w*RPW .. w*RPW + RPW - 1, in registers (p and f*h^2). A half-sweep
+// updates one colour in place (its neighbours are the other colour): row
+// neighbours within a lane's rows, column neighbours by DPP, the rows of the
+// neighbouring waves through LDS (one barrier per half-sweep).
+//
+// Groups: every RES_NS sweeps the tiles exchange their RES_HALO-deep edge
+// bands through global memory (write-through stores, one flag per tile and
+// group; each tile waits for its <= 8 neighbours only): within a group the
+// halo goes stale by one cell per half-sweep and never reaches the owned
+// cells (RES_HALO = 2 RES_NS), exactly as the fused march launches' halos.
+//
+// Stop rule: proof mode: every tile proves "the reference goes
+// on" for each iteration from its black cells' updates (max |p' - p| against
+// the proof threshold) and marks the iteration proven; a per-group arrival
+// counter says when every tile has contributed. Group g is checked at the
+// start of group g + RES_LAG (no grid barrier on the sweep path). A capped
+// solve (the BASELINE sizes) runs to the cap in this one launch; an iteration
+// no tile proves (near convergence, or non-finite values) ends the launch
+// with code 2 at the group's first iteration k0: the host replays the solve
+// to k0 from its intact input (same launch, checks off) and goes on with the
+// exact-residual launches from there (Solver::solve_resident).
+//
+// Bits: every update is sor_update<CAVITY>'s operations on the same operands
+// in the same order as tile.hip / the march kernels and the oracle's
+// red-black restatement (f*h^2 is precomputed: the same rounding), so p is
+// bit-identical to them.
+#pragma once
+
+#include "device.hpp"
+
+namespace cfd {
+
+constexpr int RES_NS = 4;                    // sweeps per group
+constexpr int RES_HALO = 2 * RES_NS;         // halo cells per side (one per half-sweep)
+constexpr int RES_TW = 128 - 2 * RES_HALO;   // owned columns per tile (112)
+constexpr int RES_MAXW = 8;                  // waves per workgroup, at most (2 per SIMD: 256 VGPRs each)
+constexpr int RES_LAG = 2;                   // group g is checked at the start of group g + RES_LAG
+constexpr int RES_REPLAY = 1;                // flags: no stop test (the host replays to a known count)
+
+struct ResPlan {
+  int ctiles, rtiles;  // column tiles (RES_TW owned columns) x row tiles (th owned rows)
+  int th;              // owned rows per tile (even)
+  int lo, hi;          // owned rows [lo, hi) of the strip (ghost rows included; lo even)
+  int waves;           // waves per workgroup (region rows th + 2 RES_HALO, rpw per wave)
+  int rpw;             // region rows per wave (template parameter of the kernel)
+};
+
+// Device state of one resident solve (zeroed before every launch: the flags
+// count groups of this launch only).
+struct ResCtl {
+  double* xa;           // edge bands of even groups (a full field, owned cells of the bands only)
+  double* xb;           // ... of odd groups
+  unsigned* flags;      // [tiles x RES_MAXW] groups each wave of each tile has completed and published
+  unsigned* proven;     // [K + 1] 1: some tile proved iteration k goes on
+  int* status;          // [0] 0 cap reached, 1 stop at [1] (only k = 0 here), 2 iteration [1] + 1 left
+                        // open (fallback); [2] != 0: a wait timed out (never expected)
+  const double* tol;    // [0] tolerance, [1] initial residual, [2] max|f| (tol_kernel)
+  int K;                // sweeps to run (the cap, or the replayed count)
+  int check_every;      // the reference tests every iteration (1)
+};
+
+// Tiling of a strip's owned rows [lo, hi) into at most max_tiles tiles, or
+// ctiles = 0 if the grid does not fit (the solver keeps the per-launch kernels)
+ResPlan res_plan(int nx, int lo, int hi, int max_tiles);
+__host__ __device__ inline int res_groups(int K) { return (K + RES_NS - 1) / RES_NS; }
+// unsigned words of flags + proofs + status, rounded to 16 B
+inline size_t res_state_words(int tiles, int K) {
+  const size_t n = (size_t)tiles * RES_MAXW + (size_t)K + 1 + 8;
+  return (n + 3) / 4 * 4;
+}
+void res_launch(int case_id, const Geo& g, const Coef& c, const double* pin, double* pout, const double* f,
+                const ResCtl& R, const ResPlan& rp, int flags, hipStream_t st);
+
+}  // namespace cfd

@@ -20,6 +20,7 @@
 #include "lexw.hpp"
 #include "small.hpp"
 #include "tile.hpp"
+#include "resident.hpp"
 #include "open.hpp"
 #include "smlex.hpp"
 #include "seqsum.hpp"
@@ -165,6 +166,26 @@ class Solver {
     tplan = tile_plan(P.nx, g.wj0, g.wj1 + 1, tile_rounds * n_cu);
     tile_on = tplan.ctiles > 0;
   }
+  // Register-resident whole-solve launch (resident.hpp): red-black cavity, one
+  // strip, no ranks, proof mode, a grid of at most one tile per CU
+  // (CFD_TUNE_RESIDENT). Its exchange fields and state words are allocated at
+  // the first solve.
+  bool res_knob = false;
+  bool res_on = false;
+  ResPlan rplan{};
+  double* res_x[2] = {nullptr, nullptr};
+  unsigned* res_state = nullptr;
+  size_t res_state_n = 0;
+  void plan_resident() {
+    res_on = false;
+    rplan = ResPlan{};
+    if (!res_knob || P.ordering != CFD_ORDER_RB || S.size() != 1 || comm || P.case_id != CFD_CAVITY || thermal ||
+        !proof_enabled || !(C.proof_k > 0.0))
+      return;
+    const Geo& g = S[0].g;
+    rplan = res_plan(P.nx, g.wj0, g.wj1 + 1, n_cu);
+    res_on = rplan.ctiles > 0;
+  }
   struct LaunchRec {
     int first, n;        // iterations first .. first+n-1
     bool proof = false;  // its ring slots hold proof ratios (proof-mode launch), not residuals
@@ -212,6 +233,7 @@ class Solver {
   void set_tuning(int knob, int v) {
     set_tuning_value(knob, v);
     if (knob == CFD_TUNE_TILE_ROUNDS) plan_tiles();
+    if (knob == CFD_TUNE_RESIDENT) plan_resident();
   }
   void set_tuning_value(int knob, int v) {
     switch (knob) {
@@ -226,6 +248,7 @@ class Solver {
       case CFD_TUNE_TILE_ROUNDS: tile_rounds = std::max(0, std::min(v, 16)); break;
       case CFD_TUNE_MARCH_ORDER: march_flags = (march_flags & ~8) | (v ? 8 : 0); break;
       case CFD_TUNE_LEXW_LEFT: lexw_left = v != 0; break;
+      case CFD_TUNE_RESIDENT: res_knob = v != 0; break;
       default: throw Error(CFD_E_ARG, "unknown tuning knob");
     }
   }
@@ -313,7 +336,8 @@ class Solver {
       // and the reference order, 24 for the red-black cavity / step; LDS tiles
       // for the cavity only
       for (int knob : {CFD_TUNE_LEXW_EDGE_PCT, CFD_TUNE_PAIR_EDGE_PCT, CFD_TUNE_MARCH_MIN_TH, CFD_TUNE_TENT_TH,
-                       CFD_TUNE_LEXW_RAMP_PCT, CFD_TUNE_TILE_ROUNDS, CFD_TUNE_MARCH_ORDER, CFD_TUNE_LEXW_LEFT}) {
+                       CFD_TUNE_LEXW_RAMP_PCT, CFD_TUNE_TILE_ROUNDS, CFD_TUNE_MARCH_ORDER, CFD_TUNE_LEXW_LEFT,
+                       CFD_TUNE_RESIDENT}) {
         int v = 0;
         if (cfd_tuning_default(&P, knob, &v) == CFD_OK) set_tuning_value(knob, v);
       }
@@ -399,6 +423,7 @@ class Solver {
       }
     }
     plan_tiles();
+    plan_resident();
     // the step's proof launches on strips / ranks: 3 sweeps (open.hip: its
     // block edge reads one row deeper than the 4-sweep pipeline's 8)
     if (P.case_id == CFD_BACKSTEP && multi()) proof_ns = 3;
@@ -469,6 +494,13 @@ class Solver {
     lexbits = nullptr;
     if (smlex_ck) (void)hipFree(smlex_ck);
     smlex_ck = nullptr;
+    for (auto*& x : res_x) {
+      if (x) (void)hipFree(x);
+      x = nullptr;
+    }
+    if (res_state) (void)hipFree(res_state);
+    res_state = nullptr;
+    res_state_n = 0;
     lexbits_words = 0;
     if (stop) (void)hipFree(stop);
     stop = nullptr;
@@ -1473,11 +1505,113 @@ class Solver {
       solve_small(out);
       return;
     }
+    if (res_on) {
+      T.sor_kernel = CFD_SOR_RESIDENT;
+      int k0 = 0;
+      if (solve_resident(out, k0)) return;
+      solve_rb(out, k0);  // an iteration the proof left open: exact launches from k0
+      return;
+    }
     T.sor_kernel = tile_on ? CFD_SOR_TILE : CFD_SOR_MARCH;
+    solve_rb(out, 0);
+  }
+
+  // The register-resident solve (resident.hpp): one persistent launch runs the
+  // whole capped solve. Returns true when the solve is done; false with k0:
+  // iteration k0 + 1's group was left open by the proof, the field after k0
+  // iterations is in the output buffer of "launch 0" (pbuf(base + 1)), and
+  // solve_rb goes on from there with exact residuals (k0 = 0: from scratch).
+  bool solve_resident(cfd_step_info* out, int& k0) {
+    Strip& s = S[0];
+    const int base = pcur;
+    const size_t fbytes = (size_t)s.g.nrows * pitch * sizeof(double);
+    double* pin = s.b[pbuf(base)];
+    double* pout = s.b[pbuf((base + 1) % nbufs())];
+    HIPC(hipMemsetAsync(pin, 0, fbytes, st));  // cavity-01.cpp:610-611: each solve starts from a zero field
+    solve_tolerance();
+    if (!res_x[0])
+      for (auto*& x : res_x) {
+        HIPC(hipMalloc(&x, fbytes));
+        HIPC(hipMemsetAsync(x, 0, fbytes, st));  // (cells outside the grid stay finite)
+      }
+    const int ntiles = rplan.ctiles * rplan.rtiles, K = P.max_iters;
+    const size_t words = res_state_words(ntiles, K);
+    if (words > res_state_n) {
+      if (res_state) HIPC(hipFree(res_state));
+      res_state = nullptr;
+      HIPC(hipMalloc(&res_state, words * sizeof(unsigned)));
+      res_state_n = words;
+    }
+    ResCtl R{};
+    R.xa = res_x[0];
+    R.xb = res_x[1];
+    R.flags = res_state;
+    R.proven = R.flags + (size_t)ntiles * RES_MAXW;
+    R.status = reinterpret_cast<int*>(R.proven + K + 1);
+    R.tol = tolv;
+    R.K = K;
+    R.check_every = std::max(1, P.check_every);
+    HIPC(hipMemsetAsync(res_state, 0, words * sizeof(unsigned), st));
+    HIPC(hipEventRecord(ev_a, st));
+    res_launch(CAVITY, s.g, C, pin, pout, s.b[B_F], R, rplan, 0, st);
+    check_launch("poisson (resident)");
+    HIPC(hipEventRecord(ev_b, st));
+    HIPC(hipMemcpyAsync(h_stat, R.status, 3 * sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    const int code = h_stat[0], kst = h_stat[1], timeout = h_stat[2];
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
+    T.poisson_ms += ms;
+    T.poisson_launches += 1;
+    if (timeout) throw Error(CFD_E_STATE, "resident SOR solve: a tile's wait timed out (tiles not co-resident?)");
+    if (code == 0 || code == 1) {
+      const int iters = code == 0 ? K : 0;
+      double res;
+      if (iters == 0) {
+        double t2[2];
+        HIPC(hipMemcpy(t2, tolv, sizeof t2, hipMemcpyDeviceToHost));
+        res = t2[1];
+      } else {
+        pcur = (base + 1) % nbufs();
+        res = final_residual(pbuf(pcur));  // the final field's (cavity-01.cpp:659-677)
+      }
+      T.poisson_sweeps += iters;
+      T.poisson_cell_updates += (long long)P.nx * P.ny * iters;
+      if (out) {
+        out->sor_iterations = iters;
+        out->residual = res;
+      }
+      return true;
+    }
+    if (code != 2 || kst < 0 || kst >= K) throw Error(CFD_E_STATE, "resident SOR solve: bad status");
+    ++T.proof_fallbacks;
+    k0 = kst;
+    if (k0 > 0) {  // the field after k0 iterations, from the solve's intact input
+      HIPC(hipMemsetAsync(res_state, 0, words * sizeof(unsigned), st));
+      R.K = k0;
+      HIPC(hipEventRecord(ev_a, st));
+      res_launch(CAVITY, s.g, C, pin, pout, s.b[B_F], R, rplan, RES_REPLAY, st);
+      check_launch("poisson (resident replay)");
+      HIPC(hipEventRecord(ev_b, st));
+      HIPC(hipMemcpyAsync(h_stat, R.status, 3 * sizeof(int), hipMemcpyDeviceToHost, st));
+      HIPC(hipStreamSynchronize(st));
+      HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
+      T.poisson_ms += ms;
+      T.poisson_launches += 1;
+      if (h_stat[2]) throw Error(CFD_E_STATE, "resident SOR replay: a tile's wait timed out");
+    }
+    return false;
+  }
+
+  // The red-black solve as a sequence of launches (march or LDS tiles). k0 > 0:
+  // iterations 1 .. k0 are done (solve_resident) and every one of them was
+  // proven to go on; their field is launch 0's output, and the solve goes on
+  // from there with one chunk of exact launches first.
+  void solve_rb(cfd_step_info* out, int k0) {
     const int base = pcur;
     HIPC(hipMemsetAsync(ring, 0, (size_t)RING * RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
     HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
-    if (P.case_id == CFD_CAVITY) {
+    if (P.case_id == CFD_CAVITY && k0 == 0) {
       // cavity-01.cpp:610-611: each solve starts from a zero field
       for (auto& s : S)
         HIPC(hipMemsetAsync(s.b[pbuf(base)], 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
@@ -1505,6 +1639,14 @@ class Solver {
     int proof_from = proof_ok() ? 0 : INT32_MAX;  // first launch (index) in proof mode
     int exact_from = 0;  // first launch whose iterations later launches test
     int iters = 0;
+    if (k0 > 0) {  // "launch 0" = the resident solve's iterations 1 .. k0 (all proven to go on)
+      launches.push_back({1, k0, true});
+      k = k0;
+      m = 1;
+      exact_from = 1;
+      last_tested = k0;
+      if (proof_from == 0) proof_from = 1 + chunk;
+    }
     auto launch_of = [&](int kk) {
       for (size_t q = 0; q < launches.size(); ++q)
         if (kk >= launches[q].first && kk <= launches[q].first + launches[q].n - 1) return (int)q;

@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 10
+#define CFD_AMD_ABI_VERSION 11
 
 /* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
  * tree (only figures): it is the cavity's projection step with a resting lid
@@ -136,8 +136,10 @@ enum cfd_sor_kernel {
   CFD_SOR_LEXW = 4,   /* reference order, multi-block march (lexw.hpp) */
   CFD_SOR_LEX = 5,    /* reference order, one workgroup, global memory (poisson_lex_kernel: step geometries
                          the other reference-order kernels do not take) */
-  CFD_SOR_SMLEX = 6   /* reference order, whole solve in one workgroup, p in LDS (smlex.hip): reference-sized
+  CFD_SOR_SMLEX = 6,  /* reference order, whole solve in one workgroup, p in LDS (smlex.hip): reference-sized
                          grids (ABI 9) */
+  CFD_SOR_RESIDENT = 7 /* red-black whole solve in one persistent launch, every tile of p in registers
+                          (resident.hpp): one strip of up to ~2 M cells (ABI 11) */
 };
 
 /* Library / ABI info. */
@@ -223,9 +225,11 @@ enum cfd_tuning {
                                  default 1 for the cavity, 0 for the open cases) */
   CFD_TUNE_MARCH_ORDER = 9,   /* red-black march launches: 0 = the column tiles of a band on consecutive waves
                                  (default), 1 = the bands of a column tile (ABI 9) */
-  CFD_TUNE_LEXW_LEFT = 10     /* reference-order backwards step: 1 = the column tiles left of the step's column end
+  CFD_TUNE_LEXW_LEFT = 10,    /* reference-order backwards step: 1 = the column tiles left of the step's column end
                                  at the block's bottom row and march as a channel below it (default), 0 = the
                                  per-cell masked march over every row that reaches the block (ABI 10) */
+  CFD_TUNE_RESIDENT = 11      /* red-black cavity, one strip, proof mode: 1 = the whole solve as one persistent
+                                 register-resident launch where the grid fits one tile per CU, 0 = never (ABI 11) */
 };
 int cfd_set_tuning(cfd_solver* s, int knob, int value);
 /* The default a solver created from these parameters starts with (host only, no

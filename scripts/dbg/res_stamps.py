@@ -1,0 +1,46 @@
+"""Group-phase cycles of the resident red-black solve (diagnostic build with
+CFD_RES_STAMPS=1, libcfd_amd_rstamps.so): one warm-up step, then one capped
+step; per wave the cycles of its neighbour waits, halo loads, first exchange,
+sweeps and group end, summed over the solve; printed per group (mean over the
+tiles' waves, and the slowest wave).
+
+usage: CFD_AMD_LIB=libcfd_amd_rstamps.so python3 scripts/dbg/res_stamps.py nx ny [max_iters]
+"""
+import ctypes
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "computational-fluid-dynamics_amd"))
+import numpy as np  # noqa: E402
+import cfd_amd as C  # noqa: E402
+from cfd_amd import _lib  # noqa: E402
+
+nx, ny = int(sys.argv[1]), int(sys.argv[2])
+iters = int(sys.argv[3]) if len(sys.argv) > 3 else 10000
+cp = C.make_params("cavity", nx=nx, ny=ny, max_iters=iters)
+s = C.CavitySolver(cp, device=0, ordering="rb", small_solve="off", tuning={"resident": 1})
+s.applyBoundaryConditions()
+s.step()
+s.reset_timing()
+s.step()
+s.synchronize()
+tm = s.timing()
+L = _lib.lib()
+n = 256 * 8 * 6
+buf = (ctypes.c_ulonglong * n)()
+L.cfd_res_stamps(buf, n)
+a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8, 6).astype(np.float64)
+groups = a[:, :, 5]
+used = groups > 0
+names = ["wait", "halo", "first_exchange", "sweeps", "end"]
+out = {"nx": nx, "ny": ny, "iters": iters, "solve_ms": tm.poisson_ms, "launches": tm.poisson_launches,
+       "fallbacks": tm.proof_fallbacks, "waves": int(used.sum()),
+       "us_per_sweep": 1000 * tm.poisson_ms / iters}
+for k, nm in enumerate(names):
+    per_group = a[:, :, k][used] / groups[used]
+    out[nm + "_cyc_per_group_mean"] = round(float(per_group.mean()), 1)
+    out[nm + "_cyc_per_group_max"] = round(float(per_group.max()), 1)
+tot = sum(a[:, :, k] for k in range(5))[used] / groups[used]
+out["total_cyc_per_group_mean"] = round(float(tot.mean()), 1)
+print(json.dumps(out, indent=1))

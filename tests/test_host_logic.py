@@ -44,7 +44,7 @@ def test_nm_exports_match_header():
 
 
 def test_abi_version():
-    assert _lib.lib().cfd_abi_version() == 10
+    assert _lib.lib().cfd_abi_version() == 11
 
 
 def test_params_struct_layout_matches_header(tmp_path):
@@ -92,7 +92,7 @@ def test_switches_default_to_auto_and_map():
     assert (lp.proof_test, lp.small_solve, lp.overlap) == (0, 0, 0)
     cp = C.solver.to_cparams(C.make_params("cavity"), proof_test="off", small_solve="on", overlap="off")
     assert (cp.proof_test, cp.small_solve, cp.overlap) == (2, 1, 2)
-    assert set(_lib.TUNING.values()) == set(range(11))
+    assert set(_lib.TUNING.values()) == set(range(12))
 
 
 @pytest.mark.parametrize("case", ["cavity", "channel", "backwards_step"])
@@ -213,7 +213,7 @@ def test_reference_order_is_the_default():
     ("cavity", "tile_rounds", 1), ("channel", "tile_rounds", 0), ("rayleigh_benard", "tile_rounds", 1),
     ("cavity", "tent_th", 64), ("channel", "lexw_edge_pct", 75), ("backwards_step", "lexw_ramp_pct", 0),
     ("cavity@4096", "lexw_edge_pct", 100), ("cavity@1024", "lexw_edge_pct", 75),
-    ("backwards_step", "lexw_left", 1), ("cavity", "lexw_left", 1),
+    ("backwards_step", "lexw_left", 1), ("cavity", "lexw_left", 1), ("cavity/rb", "resident", 0),
 ])
 def test_tuning_defaults(case, knob, value):
     """The launch-plan defaults a solver starts with (cfd_tuning_default, host
