@@ -173,7 +173,7 @@ extern "C" int cfd_tuning_default(const cfd_params* p, int knob, int* value) {
     case CFD_TUNE_TILE_ROUNDS: *value = cav ? 1 : 0; return CFD_OK;
     case CFD_TUNE_MARCH_ORDER: *value = 0; return CFD_OK;
     case CFD_TUNE_LEXW_LEFT: *value = 1; return CFD_OK;
-    case CFD_TUNE_RESIDENT: *value = 0; return CFD_OK;
+    case CFD_TUNE_RESIDENT: *value = cav ? 1 : 0; return CFD_OK;
     case CFD_TUNE_PAIR_WPS:
     case CFD_TUNE_WAVE_WPS:
     case CFD_TUNE_LEXW_WAVES:

@@ -53,62 +53,83 @@ struct ResLane {
 // rows outside the grid - per-row fix-ups (fzm: frozen rows keep their value;
 // tpm: the top row's omega / nc), no proofs. Plain waves (every row in 1 ..
 // ny - 1) record max |p' - p| of their proving black cells (lane multipliers).
-template <int RPW, int COL, bool GEN>
-__device__ __forceinline__ void res_half(const ResLane& L, double2 (&p)[RPW], const double2 (&fh)[RPW],
-                                         const double2& Sx, const double2& Nx, unsigned fzm, unsigned tpm,
-                                         double& dmx) {
-  double pc[RPW], pw[RPW], pe[RPW], sum[RPW], ns[RPW], nv[RPW];
+template <int RPW, int COL, bool GEN, int Q0, int NQ>
+__device__ __forceinline__ void res_half_block(const ResLane& L, double2 (&p)[RPW], const double2 (&fh)[RPW],
+                                               const double2& Sx, const double2& Nx, unsigned fzm, unsigned tpm,
+                                               double& dmx) {
+  double pc[NQ], pw[NQ], pe[NQ], sum[NQ], ns[NQ], nv[NQ];
 #pragma unroll
-  for (int q = 0; q < RPW; ++q) {
+  for (int k = 0; k < NQ; ++k) {
+    const int q = Q0 + k;
     if ((q & 1) == COL) {
-      pc[q] = p[q].x;
-      pw[q] = dpp_from_left(p[q].y);
-      pe[q] = p[q].y;
+      pc[k] = p[q].x;
+      pw[k] = dpp_from_left(p[q].y);
+      pe[k] = p[q].y;
     } else {
-      pc[q] = p[q].y;
-      pw[q] = p[q].x;
-      pe[q] = dpp_from_right(p[q].x);
+      pc[k] = p[q].y;
+      pw[k] = p[q].x;
+      pe[k] = dpp_from_right(p[q].x);
     }
   }
 #pragma unroll
-  for (int q = 0; q < RPW; ++q) sum[q] = pe[q] + pw[q];
+  for (int k = 0; k < NQ; ++k) sum[k] = pe[k] + pw[k];
 #pragma unroll
-  for (int q = 0; q < RPW; ++q) {
+  for (int k = 0; k < NQ; ++k) {
+    const int q = Q0 + k;
+    // (the rows below Q0 are already updated in this half-sweep: other colour
+    // cells only, the ones read here are unchanged)
     const double2 S = (q == 0) ? Sx : p[q - 1];
     const double2 N = (q == RPW - 1) ? Nx : p[q + 1];
-    ns[q] = ((q & 1) == COL) ? (N.x + S.x) : (N.y + S.y);
+    ns[k] = ((q & 1) == COL) ? (N.x + S.x) : (N.y + S.y);
   }
 #pragma unroll
-  for (int q = 0; q < RPW; ++q) sum[q] = sum[q] + ns[q];
+  for (int k = 0; k < NQ; ++k) sum[k] = sum[k] + ns[k];
 #pragma unroll
-  for (int q = 0; q < RPW; ++q) sum[q] = sum[q] - (((q & 1) == COL) ? fh[q].x : fh[q].y);
+  for (int k = 0; k < NQ; ++k) sum[k] = sum[k] - ((((Q0 + k) & 1) == COL) ? fh[Q0 + k].x : fh[Q0 + k].y);
 #pragma unroll
-  for (int q = 0; q < RPW; ++q) {
-    const bool A = (q & 1) == COL;
-    nv[q] = pc[q] * (A ? L.omm_a : L.omm_b) + (A ? L.om_a : L.om_b) * sum[q];
+  for (int k = 0; k < NQ; ++k) {
+    const bool A = ((Q0 + k) & 1) == COL;
+    nv[k] = pc[k] * (A ? L.omm_a : L.omm_b) + (A ? L.om_a : L.om_b) * sum[k];
   }
   if constexpr (GEN) {
     asm volatile("" : "+s"(fzm), "+s"(tpm));
 #pragma unroll
-    for (int q = 0; q < RPW; ++q) {
+    for (int k = 0; k < NQ; ++k) {
+      const int q = Q0 + k;
       const bool A = (q & 1) == COL;
-      if ((tpm >> q) & 1u) nv[q] = pc[q] * (A ? L.omm_a : L.omm_b) + (A ? L.omt_a : L.omt_b) * sum[q];
-      if ((fzm >> q) & 1u) nv[q] = pc[q];
+      if ((tpm >> q) & 1u) nv[k] = pc[k] * (A ? L.omm_a : L.omm_b) + (A ? L.omt_a : L.omt_b) * sum[k];
+      if ((fzm >> q) & 1u) nv[k] = pc[k];
     }
   } else if constexpr (COL == 1) {
 #pragma unroll
-    for (int q = 0; q < RPW; ++q) dmx = fmax(dmx, fabs(nv[q] - pc[q]) * (((q & 1) == COL) ? L.pa : L.pb));
+    for (int k = 0; k < NQ; ++k) dmx = fmax(dmx, fabs(nv[k] - pc[k]) * ((((Q0 + k) & 1) == COL) ? L.pa : L.pb));
   }
 #pragma unroll
-  for (int q = 0; q < RPW; ++q) {
-    if ((q & 1) == COL) p[q].x = nv[q];
-    else p[q].y = nv[q];
+  for (int k = 0; k < NQ; ++k) {
+    if (((Q0 + k) & 1) == COL) p[Q0 + k].x = nv[k];
+    else p[Q0 + k].y = nv[k];
+  }
+}
+
+// rows in scheduling blocks of RES_BLK (16-row waves: bounded live temporaries)
+#ifndef CFD_RES_BLK
+#define CFD_RES_BLK 8
+#endif
+template <int RPW, int COL, bool GEN, int Q0 = 0>
+__device__ __forceinline__ void res_half(const ResLane& L, double2 (&p)[RPW], const double2 (&fh)[RPW],
+                                         const double2& Sx, const double2& Nx, unsigned fzm, unsigned tpm,
+                                         double& dmx) {
+  constexpr int NQ = (RPW - Q0) < CFD_RES_BLK ? (RPW - Q0) : CFD_RES_BLK;
+  res_half_block<RPW, COL, GEN, Q0, NQ>(L, p, fh, Sx, Nx, fzm, tpm, dmx);
+  if constexpr (Q0 + NQ < RPW) {
+    __builtin_amdgcn_sched_barrier(0);
+    res_half<RPW, COL, GEN, Q0 + NQ>(L, p, fh, Sx, Nx, fzm, tpm, dmx);
   }
 }
 
 // bounded spin: true = gave up (the wait exceeded RES_SPIN_TICKS)
 __device__ __forceinline__ bool res_spin_expired(unsigned long long t0) {
-  __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_s_sleep(2);
   return wall_clock64() - t0 > RES_SPIN_TICKS;
 }
 
@@ -240,21 +261,23 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   const __amdgpu_buffer_rsrc_t xr[2] = {
       __builtin_amdgcn_make_buffer_rsrc(R.xa, 0, (int)((unsigned)g.nrows * P * 8u), 0x00020000),
       __builtin_amdgcn_make_buffer_rsrc(R.xb, 0, (int)((unsigned)g.nrows * P * 8u), 0x00020000)};
-  // Completion spreads one tile per group: when this wave starts group m, its
-  // neighbours' waves have finished group m - 1, theirs m - 2, ..., so every
-  // tile has finished group m - DIAM (DIAM: the tile grid's Chebyshev
-  // diameter). A tile's wave 0 publishes the proofs of group x during group
-  // x + 1 (drained before its flag x + 2), so at the start of group m the
-  // proofs of every group up to m - DIAM - 1 are published: group
-  // m - DIAM - 1 is checked then, with no counter and no grid barrier.
+  // Completion spreads one tile per group: when a tile starts group m, its
+  // neighbours have finished group m - 1, theirs m - 2, ..., so every tile has
+  // finished group m - DIAM (DIAM: the tile grid's Chebyshev diameter). A
+  // tile's wave 0 publishes the proofs of group x during group x + 1 (drained
+  // before its flag x + 2), so at the start of group m the proofs of every
+  // group up to m - DIAM - 1 are published: group m - DIAM - 1 is checked
+  // then, with no counter and no grid barrier.
   const int DIAM = max(rp.ctiles, rp.rtiles) - 1;
-  unsigned* const myflag = R.flags + (size_t)tile * RES_MAXW + w;
-  // the (tile, wave) flags this wave waits for: lane 8n + v = wave v of neighbour n (3x3 ring, centre skipped)
+  unsigned* const myflag = R.flags + tile;
+  // one flag per tile (every wave drained, then a barrier, then wave 0's lane 0
+  // stores it); wave 0's lanes 0..7 poll the 3x3 ring's (centre skipped): few
+  // pollers, so the polls do not crowd the write-through band stores
   int nflag = -1;
   {
-    const int n = lane >> 3, v = lane & 7, n9 = n < 4 ? n : n + 1;
+    const int n9 = lane < 4 ? lane : lane + 1;
     const int tr = rt + n9 / 3 - 1, tc = ct + n9 % 3 - 1;
-    if (v < NW && tr >= 0 && tr < rp.rtiles && tc >= 0 && tc < rp.ctiles) nflag = (tr * rp.ctiles + tc) * RES_MAXW + v;
+    if (lane < 8 && tr >= 0 && tr < rp.rtiles && tc >= 0 && tc < rp.ctiles) nflag = tr * rp.ctiles + tc;
   }
   auto wait_nb = [&](unsigned e) -> bool {  // false: gave up
     const unsigned long long t0 = wall_clock64();
@@ -298,21 +321,22 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   int pend_g = -1;  // (wave 0) the group whose proofs were loaded at this group's start
   for (int gi = 0; gi < G; ++gi) {
     const int nsw = min(NS, K - gi * NS);
-    // ---- group start: the neighbours' edge bands of group gi - 1 (each wave waits for its own)
+    // ---- group start: the neighbours' edge bands of group gi - 1 (wave 0 waits, the others after a barrier)
     if (gi > 0) {
-      const bool ok = wait_nb((unsigned)gi);
+      if (w == 0 && !wait_nb((unsigned)gi) && lane == 0) dec = 2;
       RES_STAMP(0);
-      if (!ok) {
-        dec = 2;
-      } else {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (the loads stay after the poll)
-        const __amdgpu_buffer_rsrc_t xp = xr[(gi - 1) & 1];
+      __syncthreads();
+      if (dec == 2) {  // a wait gave up: report, leave p_out alone
+        if (threadIdx.x == 0) __hip_atomic_store(R.status + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (the loads stay after the poll)
+      const __amdgpu_buffer_rsrc_t xp = xr[(gi - 1) & 1];
 #pragma unroll
-        for (int q = 0; q < RPW; ++q) {
-          const bool hrow = (haloh >> q) & 1u;
-          const bool orow = (ownm >> q) & 1u;
-          if ((hrow && col_in) || (orow && halo_lane)) p[q] = ld_sc1(xp, offs(jb + q));
-        }
+      for (int q = 0; q < RPW; ++q) {
+        const bool hrow = (haloh >> q) & 1u;
+        const bool orow = (ownm >> q) & 1u;
+        if ((hrow && col_in) || (orow && halo_lane)) p[q] = ld_sc1(xp, offs(jb + q));
       }
     }
     pend_g = -1;
@@ -342,15 +366,6 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       par ^= 1;
     };
     exchange();
-    // decisions taken at the previous group's end (a timeout now), visible after the barrier
-    if (dec == 2) {
-      if (threadIdx.x == 0) __hip_atomic_store(R.status + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    if (dec == 1) {
-      gfail = gdec;
-      break;
-    }
     if (w == 0 && !replay && gi > 0) publish_proofs(gi - 1);  // (red[] of group gi - 1: written before the barrier)
     RES_STAMP(2);
     auto sweeps = [&](auto gen_c) {
@@ -395,11 +410,16 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       dec = 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the bands (and wave 0's proofs) drained before the flag
-    if (lane == 0) __hip_atomic_store(myflag, (unsigned)(gi + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(myflag, (unsigned)(gi + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     RES_STAMP(4);
 #if CFD_RES_STAMPS
     st_acc[5] += 1;
 #endif
+    if (dec == 1) {  // (every tile decides this at the same group)
+      gfail = gdec;
+      break;
+    }
   }
 #if CFD_RES_STAMPS
   if (lane < RES_STAMP_SEGS && tile < 256) {
@@ -424,7 +444,7 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       for (int t0i = 0; t0i < ntiles && d == 0; t0i += 64) {
         const int t = t0i + lane;
         for (;;) {
-          const bool ok = t >= ntiles || ld_flag(R.flags + (size_t)t * RES_MAXW) >= (unsigned)(G + 1);
+          const bool ok = t >= ntiles || ld_flag(R.flags + t) >= (unsigned)(G + 1);
           if (__all(ok)) break;
           if (res_spin_expired(t0)) {
             d = 2;

@@ -68,7 +68,7 @@ struct ResPlan {
 struct ResCtl {
   double* xa;           // edge bands of even groups (a full field, owned cells of the bands only)
   double* xb;           // ... of odd groups
-  unsigned* flags;      // [tiles x RES_MAXW] groups each wave of each tile has completed and published
+  unsigned* flags;      // [tiles] groups each tile has completed and published
   unsigned* proven;     // [K + 1] 1: some tile proved iteration k goes on
   int* status;          // [0] 0 cap reached, 1 stop at [1] (only k = 0 here), 2 iteration [1] + 1 left
                         // open (fallback); [2] != 0: a wait timed out (never expected)
@@ -83,7 +83,7 @@ ResPlan res_plan(int nx, int lo, int hi, int max_tiles);
 __host__ __device__ inline int res_groups(int K) { return (K + RES_NS - 1) / RES_NS; }
 // unsigned words of flags + proofs + status, rounded to 16 B
 inline size_t res_state_words(int tiles, int K) {
-  const size_t n = (size_t)tiles * RES_MAXW + (size_t)K + 1 + 8;
+  const size_t n = (size_t)tiles + (size_t)K + 1 + 8;
   return (n + 3) / 4 * 4;
 }
 void res_launch(int case_id, const Geo& g, const Coef& c, const double* pin, double* pout, const double* f,

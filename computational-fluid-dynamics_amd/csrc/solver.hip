@@ -1546,7 +1546,7 @@ class Solver {
     R.xa = res_x[0];
     R.xb = res_x[1];
     R.flags = res_state;
-    R.proven = R.flags + (size_t)ntiles * RES_MAXW;
+    R.proven = R.flags + ntiles;
     R.status = reinterpret_cast<int*>(R.proven + K + 1);
     R.tol = tolv;
     R.K = K;

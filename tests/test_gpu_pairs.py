@@ -25,7 +25,7 @@ from test_gpu_parity import assert_bits  # noqa: E402
 # These are tests of the wave-march launch plan: reference-sized grids would
 # otherwise take the one-workgroup solve (small.hpp, tests/test_gpu_small.py)
 # or the LDS-tile launches (tile.hpp, tests/test_gpu_tile.py).
-MULTI = {"small_solve": "off", "tuning": {"tile_rounds": 0}}
+MULTI = {"small_solve": "off", "tuning": {"tile_rounds": 0, "resident": 0}}
 
 
 SOLVERS = {"cavity": C.CavitySolver, "channel": C.ChannelSolver, "backwards_step": C.BackwardsStepSolver}

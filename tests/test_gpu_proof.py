@@ -22,7 +22,7 @@ import oracle as O  # noqa: E402
 from test_gpu_parity import assert_bits  # noqa: E402
 
 FIELDS = ("p", "u", "v")
-MARCH = {"tile_rounds": 0}  # the wave-march launches (proof mode runs there), not the LDS tiles
+MARCH = {"tile_rounds": 0, "resident": 0}  # the wave-march launches (proof mode runs there), not the LDS tiles
 
 
 def run(monkeypatch, cp, steps, proof, ns=3, last_timing=False, **kw):

@@ -188,7 +188,7 @@ def test_open_proof_mode_on_ranks(case, world, nx, ny, steps, cap):
     and all-reduced, a re-association)."""
     kw = {"max_iters": cap} if cap else {}
     cp = C.make_params(case, nx=nx, ny=ny, **kw)
-    s, its = single(cp, steps, small_solve="off", proof_test="off", tuning={"tile_rounds": 0})
+    s, its = single(cp, steps, small_solve="off", proof_test="off", tuning={"tile_rounds": 0, "resident": 0})
     ref = {n: s.field(n) for n in ("u", "v", "p")}
     res = run_ranks(cp, world, steps, proof_test="on")
     for r in res:

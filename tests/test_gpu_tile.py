@@ -28,11 +28,11 @@ TILE_W = 108  # owned columns per tile (tile.hpp)
 
 # the open cases run the wave march by default (faster there since the
 # unchecked-group march); these tests ask for the tiles explicitly
-TILES = {"tile_rounds": 1}
+TILES = {"tile_rounds": 1, "resident": 0}
 
 
 def run(case, cp, steps, tile_rounds=None, **kw):
-    tuning = {"tile_rounds": 1 if tile_rounds is None else tile_rounds}
+    tuning = {"tile_rounds": 1 if tile_rounds is None else tile_rounds, "resident": 0}
     g = SOLVERS[case](cp, ordering="rb", device=0, small_solve="off", tuning=tuning, **kw)
     if case == "cavity":
         g.applyBoundaryConditions()
@@ -117,7 +117,7 @@ def test_tile_stop_inside_launch_and_explicit_sweeps(spl):
     """Converging solves (the reference's 63^2 cavity on the tile path): stops
     inside a launch are replayed from the launch's input; any sweep count."""
     cp = C.reference_defaults("cavity")
-    g = C.CavitySolver(cp, ordering="rb", device=0, small_solve="off", sweeps_per_launch=spl)
+    g = C.CavitySolver(cp, ordering="rb", device=0, small_solve="off", sweeps_per_launch=spl, tuning=TILES)
     o = O.Oracle(cp, ordering=O.RB)
     for _ in range(3):
         assert g.step() == o.step()
@@ -181,7 +181,7 @@ def test_tile_proof_mode_equals_exact(case, nx, ny, cap, tolf):
 def test_tile_proof_vs_oracle_converging():
     """The reference's 63^2 cavity on proof-mode tiles vs the red-black oracle."""
     cp = C.reference_defaults("cavity")
-    g = C.CavitySolver(cp, ordering="rb", device=0, small_solve="off")
+    g = C.CavitySolver(cp, ordering="rb", device=0, small_solve="off", tuning=TILES)
     o = O.Oracle(cp, ordering=O.RB)
     for _ in range(4):
         assert g.step() == o.step()
