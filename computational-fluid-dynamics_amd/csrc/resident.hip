@@ -1,5 +1,6 @@
-// resident.hip — the register-resident red-black SOR solve (resident.hpp has
-// the design). Own translation unit: device.hpp only.
+// resident.hip — the register-resident SOR solve (resident.hpp has the
+// design): red-black with the proof-mode stop rule, and the reference's own
+// order with sampled exceedance bits. Own translation unit: device.hpp only.
 #include <algorithm>
 #include <type_traits>
 
@@ -53,10 +54,30 @@ struct ResLane {
 // rows outside the grid - per-row fix-ups (fzm: frozen rows keep their value;
 // tpm: the top row's omega / nc), no proofs. Plain waves (every row in 1 ..
 // ny - 1) record max |p' - p| of their proving black cells (lane multipliers).
-template <int RPW, int COL, bool GEN, int Q0, int NQ>
+// The reference's order (LEX): cell (j, i) performs its k-th update in
+// half-sweep H = i + j + 2(k - 1) (lexw.hpp has the derivation), so a
+// half-sweep updates one colour, like red-black, among the cells whose window
+// i + j <= H <= i + j + 2(K - 1) holds it (MASK: per-cell selects; groups
+// wholly inside every window run unmasked, groups outside all of them skip).
+// Its stop rule needs, per iteration, whether some cell's residual exceeds
+// tol: one sampled row per wave (RES_QS, owned interior cells) evaluates the
+// residual of the other colour's cells in the half-sweep after their update -
+// W, S before and E, N after this half-sweep's update, exactly the reference's
+// operands (residual_interior<CAVITY>) - and records an exceedance.
+constexpr int RES_QS = 3;  // the sampled row of a wave (odd: a sweep's two samples share one iteration)
+struct LexHalf {
+  int u0;          // H - gx - jb: cell (row q, slot a) active iff (unsigned)(u0 - q) <= span; slot b: u0 - q - 1
+  unsigned span;   // 2 (K - 1)
+  int ks;          // the iteration of this lane's sampled cell in this half-sweep
+  unsigned kspan;  // K - 2: sampled iterations 1 .. K - 1 (the cap's is never tested)
+  double tol, idx2;
+  double2 fs;      // the source of the sampled row
+};
+
+template <int RPW, int COL, bool GEN, bool MASK, bool LEX, int Q0, int NQ>
 __device__ __forceinline__ void res_half_block(const ResLane& L, double2 (&p)[RPW], const double2 (&fh)[RPW],
                                                const double2& Sx, const double2& Nx, unsigned fzm, unsigned tpm,
-                                               double& dmx) {
+                                               double& dmx, const LexHalf& lh, bool& ex) {
   double pc[NQ], pw[NQ], pe[NQ], sum[NQ], ns[NQ], nv[NQ];
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
@@ -100,7 +121,37 @@ __device__ __forceinline__ void res_half_block(const ResLane& L, double2 (&p)[RP
       if ((tpm >> q) & 1u) nv[k] = pc[k] * (A ? L.omm_a : L.omm_b) + (A ? L.omt_a : L.omt_b) * sum[k];
       if ((fzm >> q) & 1u) nv[k] = pc[k];
     }
-  } else if constexpr (COL == 1) {
+  }
+  if constexpr (MASK) {  // the reference order's windows (ramps)
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int q = Q0 + k;
+      const unsigned u = (unsigned)(lh.u0 - q - (((q & 1) == COL) ? 0 : 1));
+      nv[k] = (u <= lh.span) ? nv[k] : pc[k];
+    }
+  }
+  if constexpr (LEX && !GEN && Q0 <= RES_QS - 1 && Q0 + NQ >= RES_QS + 2) {
+    // sampled residual of the other colour's cell c of row RES_QS (iteration
+    // lh.ks): W, S before this half-sweep's update, E, N after it
+    constexpr int kq = RES_QS - Q0;
+    double cv, W, E, fc, mult;
+    if constexpr (COL == 1) {  // row RES_QS (odd) updates slot a: c = slot b
+      cv = p[RES_QS].y;
+      W = pc[kq];
+      E = dpp_from_right(nv[kq]);
+      fc = lh.fs.y;
+      mult = L.pb;
+    } else {  // row RES_QS updates slot b: c = slot a
+      cv = p[RES_QS].x;
+      W = dpp_from_left(pc[kq]);
+      E = nv[kq];
+      fc = lh.fs.x;
+      mult = L.pa;
+    }
+    const double S = pc[kq - 1], N = nv[kq + 1];  // (rows RES_QS -+ 1 update c's column)
+    const double r = fabs(lh.idx2 * ((E - cv) + (W - cv) + (N - cv) + (S - cv)) - fc);
+    ex = ex || (r > lh.tol && mult != 0.0 && (unsigned)(lh.ks - 1) <= lh.kspan);
+  } else if constexpr (!LEX && !GEN && COL == 1) {
 #pragma unroll
     for (int k = 0; k < NQ; ++k) dmx = fmax(dmx, fabs(nv[k] - pc[k]) * ((((Q0 + k) & 1) == COL) ? L.pa : L.pb));
   }
@@ -115,16 +166,30 @@ __device__ __forceinline__ void res_half_block(const ResLane& L, double2 (&p)[RP
 #ifndef CFD_RES_BLK
 #define CFD_RES_BLK 8
 #endif
-template <int RPW, int COL, bool GEN, int Q0 = 0>
+template <int RPW, int COL, bool GEN, bool MASK, bool LEX, int Q0 = 0>
 __device__ __forceinline__ void res_half(const ResLane& L, double2 (&p)[RPW], const double2 (&fh)[RPW],
                                          const double2& Sx, const double2& Nx, unsigned fzm, unsigned tpm,
-                                         double& dmx) {
+                                         double& dmx, const LexHalf& lh, bool& ex) {
   constexpr int NQ = (RPW - Q0) < CFD_RES_BLK ? (RPW - Q0) : CFD_RES_BLK;
-  res_half_block<RPW, COL, GEN, Q0, NQ>(L, p, fh, Sx, Nx, fzm, tpm, dmx);
+  res_half_block<RPW, COL, GEN, MASK, LEX, Q0, NQ>(L, p, fh, Sx, Nx, fzm, tpm, dmx, lh, ex);
   if constexpr (Q0 + NQ < RPW) {
     __builtin_amdgcn_sched_barrier(0);
-    res_half<RPW, COL, GEN, Q0 + NQ>(L, p, fh, Sx, Nx, fzm, tpm, dmx);
+    res_half<RPW, COL, GEN, MASK, LEX, Q0 + NQ>(L, p, fh, Sx, Nx, fzm, tpm, dmx, lh, ex);
   }
+}
+
+// OR across the wave's 64 lanes
+__device__ __forceinline__ unsigned long long wave_or64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned lo = (unsigned)v, hi = (unsigned)(v >> 32);
+    v |= (unsigned long long)(unsigned)__shfl_xor((int)lo, off, 64) |
+         ((unsigned long long)(unsigned)__shfl_xor((int)hi, off, 64) << 32);
+  }
+  return v;
+}
+__device__ __forceinline__ unsigned long long ld_bits(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // bounded spin: true = gave up (the wait exceeded RES_SPIN_TICKS)
@@ -159,21 +224,22 @@ __device__ unsigned long long res_stamp_buf[256 * RES_MAXW * RES_STAMP_SEGS];
 #define RES_STAMP(seg) ((void)0)
 #endif
 
-// One launch = the whole solve (or its replay to a known count: RES_REPLAY).
-template <int RPW>
+// One launch = the whole solve (or, red-black, its replay to a known count:
+// RES_REPLAY). LEX: the reference's order.
+template <int RPW, bool LEX>
 __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo g, Coef c, const double* __restrict__ pin,
                                                                              double* __restrict__ pout,
                                                                              const double* __restrict__ f, ResCtl R,
                                                                              ResPlan rp, int flags) {
   constexpr int NS = RES_NS, H = RES_HALO, TW = RES_TW;
   __shared__ double2 E[2][RES_MAXW][2][64];  // the waves' first / last rows after each half-sweep (by parity)
-  __shared__ double red[RES_MAXW][NS + 1];   // per wave: max |p' - p| per sweep, max |p| of the group's input
+  __shared__ double red[RES_MAXW][NS + 1];   // red-black: per wave max |p' - p| per sweep, max |p| of the input
   __shared__ int dec;                         // 0 go on, 1 exit (fallback / stop), 2 exit (timeout)
-  __shared__ int gdec;                        // the group a fallback starts at
+  __shared__ int gdec;                        // red-black: the group a fallback starts at; LEX: the open iteration
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int NW = rp.waves;
-  const bool replay = (flags & RES_REPLAY) != 0;
+  const bool replay = !LEX && (flags & RES_REPLAY) != 0;
   if (threadIdx.x == 0) dec = 0;  // (read after the first barrier)
 
   // tiles of one XCD next to each other (speed only: blocks b and b + 8 share one)
@@ -188,7 +254,8 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   const int y0 = rp.lo + rt * rp.th, y1 = min(y0 + rp.th, rp.hi);  // owned rows [y0, y1)
   const int gy0 = y0 - H;                    // grid row of region row 0 (even)
   const int RR = (y1 - y0) + 2 * H;          // region rows (<= NW * RPW: host plan)
-  const int gx = x0 - H + 2 * lane;          // this lane's columns gx, gx + 1 (gx even)
+  const int c0 = x0 - H;                     // grid column of lane 0's slot a
+  const int gx = c0 + 2 * lane;              // this lane's columns gx, gx + 1 (gx even)
   const int jb = gy0 + w * RPW;              // grid row of this wave's row 0
   const int rlo = g.row_lo, rhi = g.row_lo + g.nrows - 1;  // stored rows
   const int gxc = min(max(gx, 0), g.pitch - 2);
@@ -237,8 +304,9 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
 
   // the region from p_in (rows / columns clamped to stored memory: clamped
   // cells lie outside the grid, are never updated and never stored), the
-  // source as f * h^2
+  // source as f * h^2 (LEX: the sampled row's source itself too)
   double2 p[RPW], fh[RPW];
+  LexHalf lh{};
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     const int jc = min(max(jb + q, rlo), rhi);
@@ -246,6 +314,7 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     p[q] = *reinterpret_cast<const double2*>(pin + o);
     const double2 F = *reinterpret_cast<const double2*>(f + o);
     fh[q] = make_double2(F.x * c.h2, F.y * c.h2);
+    if (LEX && q == RES_QS) lh.fs = F;
   }
   const double tol = R.tol[0];
   // the reference's loop tests the initial residual first (cavity-01.cpp:633)
@@ -257,18 +326,37 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     return;
   }
   const double fmx = R.tol[2];
-  const int K = R.K, G = res_groups(K);
+  const int K = R.K;
+  // groups: red-black NS sweeps each; LEX: NS half-sweep pairs of the skewed
+  // solve, half-sweeps H = 2 .. nx + ny + 2(K - 1) (cell (ny, nx)'s K-th update)
+  const int G = LEX ? (nx + ny + 2 * K - 3 + 2 * NS - 1) / (2 * NS) : res_groups(K);
+  lh.span = 2u * (unsigned)(K - 1);
+  lh.kspan = (unsigned)(K - 2);
+  lh.tol = tol;
+  lh.idx2 = c.idx2;
+  const int js = jb + RES_QS;  // (LEX) this wave's sampled grid row
+  // LEX: the cells of the region that can change (grid interior): their i + j range
+  const int smin = max(gy0, 1) + max(c0, 1);
+  const int smax = min(gy0 + RR - 1, ny) + min(c0 + 127, nx);
   const __amdgpu_buffer_rsrc_t xr[2] = {
       __builtin_amdgcn_make_buffer_rsrc(R.xa, 0, (int)((unsigned)g.nrows * P * 8u), 0x00020000),
       __builtin_amdgcn_make_buffer_rsrc(R.xb, 0, (int)((unsigned)g.nrows * P * 8u), 0x00020000)};
   // Completion spreads one tile per group: when a tile starts group m, its
   // neighbours have finished group m - 1, theirs m - 2, ..., so every tile has
-  // finished group m - DIAM (DIAM: the tile grid's Chebyshev diameter). A
-  // tile's wave 0 publishes the proofs of group x during group x + 1 (drained
-  // before its flag x + 2), so at the start of group m the proofs of every
-  // group up to m - DIAM - 1 are published: group m - DIAM - 1 is checked
-  // then, with no counter and no grid barrier.
+  // finished group m - DIAM (DIAM: the tile grid's Chebyshev diameter).
+  // Red-black: a tile's wave 0 publishes the proofs of group x during group
+  // x + 1 (drained before its flag x + 2), so at the start of group m the
+  // proofs of every group up to m - DIAM - 1 are published: group
+  // m - DIAM - 1 is checked then, with no counter and no grid barrier. LEX:
+  // the exceedance bits of group x are drained before the tile's flag x + 1;
+  // an iteration k has all its samples once the last cell evaluated it
+  // (half-sweep nx + ny + 2k - 1), so at the start of group m every iteration
+  // up to kdone(m - DIAM) is checked.
   const int DIAM = max(rp.ctiles, rp.rtiles) - 1;
+  auto kdone = [&](int gq) {  // the last iteration whose samples are complete after group gq
+    const int a = 2 * NS * (gq + 1) + 2 - nx - ny;
+    return a >= 0 ? a / 2 : -((-a + 1) / 2);
+  };
   unsigned* const myflag = R.flags + tile;
   // one flag per tile (every wave drained, then a barrier, then wave 0's lane 0
   // stores it); wave 0's lanes 0..7 poll the 3x3 ring's (centre skipped): few
@@ -287,7 +375,7 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       if (res_spin_expired(t0)) return false;
     }
   };
-  // proofs of group gq (wave 0): lanes < nsw store "iteration gq*NS + 1 + lane goes on"
+  // red-black: proofs of group gq (wave 0): lanes < nsw store "iteration gq*NS + 1 + lane goes on"
   auto publish_proofs = [&](int gq) {
     const int nq = min(NS, K - gq * NS);
     double dm = 0.0, pv = 0.0;
@@ -304,23 +392,41 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     if (lane < nq && ratio > 1.0)
       __hip_atomic_store(R.proven + gq * NS + 1 + lane, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  // the reference's while condition for the tested iterations of group gc
-  // (every one but the cap, which the loop never tests): lane-wise loads
+  // red-black: the reference's while condition for the tested iterations of
+  // group gc (every one but the cap, which the loop never tests): lane-wise loads
   auto check_load = [&](int gc) -> bool {
     const int kk = gc * NS + 1 + lane;
     const bool tested = lane < NS && kk <= K - 1 && kk % R.check_every == 0;
     return !tested || ld_flag(R.proven + kk) != 0u;
+  };
+  // LEX: iterations k0 .. k0 + 7 (<= klast), lane = 8 * (k - k0) + shard:
+  // this lane's shard has k's bit (every tested k needs one in some shard)
+  auto lex_load = [&](int k0, int klast) -> bool {
+    const int k = k0 + (lane >> 3), sh = lane & 7;
+    if (k > klast || k % R.check_every != 0) return true;
+    const int b = k + R.koff;
+    return (ld_bits(R.bits + (size_t)sh * R.bwords + (b >> 6)) >> (b & 63)) & 1ull;
+  };
+  // the first of k0 .. k0 + 7 (<= klast) with no bit in any shard, or -1
+  auto lex_first_open = [&](bool have, int k0, int klast) -> int {
+    const unsigned long long m = __ballot(have);
+    for (int t = 0; t < 8 && k0 + t <= klast; ++t)
+      if (((m >> (8 * t)) & 0xffull) == 0ull) return k0 + t;
+    return -1;
   };
 
 #if CFD_RES_STAMPS
   unsigned long long st_acc[RES_STAMP_SEGS] = {}, st_last;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
 #endif
-  int gfail = -1;  // first group left open (fallback)
+  int gfail = -1;  // red-black: first group left open (fallback); LEX: the open iteration
   bool pend = true;
-  int pend_g = -1;  // (wave 0) the group whose proofs were loaded at this group's start
+  int pend_g = -1;  // (wave 0) red-black: the group whose proofs were loaded at this group's start
+  int kc = 0;       // (LEX) iterations 1 .. kc checked
+  int pk0 = 0, pk1 = -1;  // (wave 0, LEX) the iterations loaded at this group's start
   for (int gi = 0; gi < G; ++gi) {
-    const int nsw = min(NS, K - gi * NS);
+    const int nsw = LEX ? NS : min(NS, K - gi * NS);
+    const int Hg = 2 + 2 * NS * gi;  // (LEX) the group's first half-sweep
     // ---- group start: the neighbours' edge bands of group gi - 1 (wave 0 waits, the others after a barrier)
     if (gi > 0) {
       if (w == 0 && !wait_nb((unsigned)gi) && lane == 0) dec = 2;
@@ -340,15 +446,25 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       }
     }
     pend_g = -1;
-    if (w == 0 && !replay && gi - DIAM - 1 >= 0) {  // evaluated at this group's end
+    if constexpr (LEX) {  // the iterations every tile has finished sampling (evaluated at this group's end)
+      pk1 = -1;
+      const int kd = min(K - 1, kdone(gi - DIAM));
+      if (w == 0 && gi - DIAM >= 0 && kd > kc) {
+        pk0 = kc + 1;
+        pk1 = min(kd, kc + 8);
+        pend = lex_load(pk0, pk1);
+      }
+    } else if (w == 0 && !replay && gi - DIAM - 1 >= 0) {  // evaluated at this group's end
       pend_g = gi - DIAM - 1;
       pend = check_load(pend_g);
     }
-    // max |p| over the region: the proof's P of this group's sweeps
+    // max |p| over the region: the proof's P of this group's sweeps (red-black)
     double pm = 0.0;
+    if constexpr (!LEX) {
 #pragma unroll
-    for (int q = 0; q < RPW; ++q)
-      if ((rowm >> q) & 1u) pm = fmax(pm, fmax(fabs(p[q].x), fabs(p[q].y)));
+      for (int q = 0; q < RPW; ++q)
+        if ((rowm >> q) & 1u) pm = fmax(pm, fmax(fabs(p[q].x), fabs(p[q].y)));
+    }
 #if CFD_RES_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the halo loads' latency in phase 1)
 #endif
@@ -356,6 +472,7 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     // ---- NS sweeps (red, black), the waves' edge rows through LDS after each half-sweep
     double2 Sx = make_double2(0.0, 0.0), Nx = Sx;
     double dmx[NS];
+    unsigned long long exm = 0ull;  // (LEX) bit s: a sampled residual of sweep s exceeds tol
     int par = 0;
     auto exchange = [&]() {
       E[par][w][0][lane] = p[0];
@@ -365,27 +482,67 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       if (w < NW - 1) Nx = E[par][w + 1][0][lane];
       par ^= 1;
     };
-    exchange();
-    if (w == 0 && !replay && gi > 0) publish_proofs(gi - 1);  // (red[] of group gi - 1: written before the barrier)
+    // LEX: the group's activity class (tile-uniform): 0 no cell active in any
+    // of its half-sweeps, 1 some (masked), 2 every cell in every one
+    int act = 2;
+    if constexpr (LEX) {
+      const int He = Hg + 2 * NS - 1;
+      act = (He < smin || Hg - smax > (int)lh.span) ? 0 : (Hg - smax >= 0 && He - smin <= (int)lh.span) ? 2 : 1;
+    }
+    if (act != 0) exchange();
+    if (w == 0 && !replay && !LEX && gi > 0) publish_proofs(gi - 1);  // (red[] of group gi - 1: before the barrier)
     RES_STAMP(2);
-    auto sweeps = [&](auto gen_c) {
+    auto sweeps = [&](auto gen_c, auto mask_c) {
       constexpr bool GEN = decltype(gen_c)::value;
+      constexpr bool MASK = decltype(mask_c)::value;
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         dmx[s] = 0.0;
         if (s < nsw) {
-          res_half<RPW, 0, GEN>(L, p, fh, Sx, Nx, fzm, tpm, dmx[s]);
+          bool ex = false;
+          if constexpr (LEX) {
+            lh.u0 = Hg + 2 * s - gx - jb;
+            lh.ks = (Hg + 2 * s - 1 - gx - js) / 2 + 1;
+          }
+          res_half<RPW, 0, GEN, MASK, LEX>(L, p, fh, Sx, Nx, fzm, tpm, dmx[s], lh, ex);
           exchange();
-          res_half<RPW, 1, GEN>(L, p, fh, Sx, Nx, fzm, tpm, dmx[s]);
+          if constexpr (LEX) lh.u0 += 1;
+          res_half<RPW, 1, GEN, MASK, LEX>(L, p, fh, Sx, Nx, fzm, tpm, dmx[s], lh, ex);
           if (s + 1 < nsw) exchange();
+          if constexpr (LEX) exm |= ex ? (1ull << s) : 0ull;
         }
       }
     };
-    if (gen) sweeps(std::true_type{});
-    else sweeps(std::false_type{});
+    if (LEX && act == 1) {
+      if (gen) sweeps(std::true_type{}, std::true_type{});
+      else sweeps(std::false_type{}, std::true_type{});
+    } else if (act != 0) {
+      if (gen) sweeps(std::true_type{}, std::false_type{});
+      else sweeps(std::false_type{}, std::false_type{});
+    }
     RES_STAMP(3);
-    // ---- group end: this wave's proof values, its part of the edge bands, its flag
-    if (!replay) {
+    // ---- group end: this wave's proof values / exceedance bits, its part of the edge bands, its flag
+    if constexpr (LEX) {
+      // lane l's bit s <-> iteration kw - l + s (kw: lane 0's sampled iteration
+      // at sweep 0): shift by 63 - l into a 128-bit run, OR the lanes
+      const int kw = (Hg - 1 - c0 - js) / 2 + 1;
+      const int sh = 63 - lane;
+      const unsigned long long lo = exm << sh, hi = sh ? (exm >> (64 - sh)) : 0ull;
+      const unsigned long long b0 = wave_or64(lo), b1 = wave_or64(hi);
+      if (lane == 0 && (b0 | b1) != 0ull) {
+        unsigned long long* Bs = R.bits + (size_t)(tile & 7) * R.bwords;
+        const int q0 = kw - 63 + R.koff;  // (>= 0: koff covers the earliest cells)
+        const int wd = q0 >> 6, o = q0 & 63;
+        if (b0) {
+          atomicOr(Bs + wd, b0 << o);
+          if (o) atomicOr(Bs + wd + 1, b0 >> (64 - o));
+        }
+        if (b1) {
+          atomicOr(Bs + wd + 1, b1 << o);
+          if (o) atomicOr(Bs + wd + 2, b1 >> (64 - o));
+        }
+      }
+    } else if (!replay) {
 #pragma unroll
       for (int s = 0; s < NS; ++s) dmx[s] = wave_max(dmx[s]);
       pm = wave_max(pm);
@@ -405,11 +562,20 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
         if (orow && own_pair && (brow || band_lane)) st_sc1(xo, offs(j), p[q]);
       }
     }
-    if (pend_g >= 0 && !__all(pend) && lane == 0) {  // (wave 0) group pend_g left an iteration open
+    if constexpr (LEX) {
+      if (w == 0 && pk1 >= pk0) {
+        const int ko = lex_first_open(pend, pk0, pk1);
+        if (ko >= 0 && lane == 0) {  // iteration ko: no sampled cell exceeds tol (left open)
+          gdec = ko;
+          dec = 1;
+        }
+        kc = pk1;
+      }
+    } else if (pend_g >= 0 && !__all(pend) && lane == 0) {  // (wave 0) group pend_g left an iteration open
       gdec = pend_g;
       dec = 1;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the bands (and wave 0's proofs) drained before the flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the bands (and wave 0's proofs / bits) drained before the flag
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(myflag, (unsigned)(gi + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     RES_STAMP(4);
@@ -430,21 +596,24 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   }
 #endif
   if (gfail < 0 && !replay) {
-    // the groups the loop did not check: every tile's last proofs published
-    // (wave 0's flag G + 1), then groups max(0, G - DIAM - 1) .. G - 1 in order
-    __syncthreads();  // (red[] of the last group; dec of the last check)
-    if (dec == 1) {
-      gfail = gdec;
-    } else if (w == 0) {
+    // what the loop did not check, once every tile has published everything
+    // (red-black: wave 0's flag G + 1 after its last proofs; LEX: flag G):
+    // red-black groups max(0, G - DIAM - 1) .. G - 1, LEX iterations kc + 1 .. K - 1
+    __syncthreads();  // (red[] of the last group)
+    if (w == 0) {
       int d = 0;
-      publish_proofs(G - 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(myflag, (unsigned)(G + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned want = (unsigned)G;
+      if constexpr (!LEX) {
+        publish_proofs(G - 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(myflag, (unsigned)(G + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        want = (unsigned)(G + 1);
+      }
       const unsigned long long t0 = wall_clock64();
       for (int t0i = 0; t0i < ntiles && d == 0; t0i += 64) {
         const int t = t0i + lane;
         for (;;) {
-          const bool ok = t >= ntiles || ld_flag(R.flags + t) >= (unsigned)(G + 1);
+          const bool ok = t >= ntiles || ld_flag(R.flags + t) >= want;
           if (__all(ok)) break;
           if (res_spin_expired(t0)) {
             d = 2;
@@ -453,11 +622,21 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      for (int gc = max(0, G - DIAM - 1); gc < G && d == 0; ++gc)
-        if (!__all(check_load(gc))) {
-          d = 1;
-          if (lane == 0) gdec = gc;
+      if constexpr (LEX) {
+        for (int k0 = kc + 1; k0 <= K - 1 && d == 0; k0 += 8) {
+          const int ko = lex_first_open(lex_load(k0, K - 1), k0, K - 1);
+          if (ko >= 0) {
+            d = 1;
+            if (lane == 0) gdec = ko;
+          }
         }
+      } else {
+        for (int gc = max(0, G - DIAM - 1); gc < G && d == 0; ++gc)
+          if (!__all(check_load(gc))) {
+            d = 1;
+            if (lane == 0) gdec = gc;
+          }
+      }
       if (lane == 0) dec = d;
     }
     __syncthreads();
@@ -467,10 +646,10 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       return;
     }
   }
-  if (gfail >= 0) {  // the host replays to gfail * NS and evaluates from there
+  if (gfail >= 0) {  // red-black: the host replays to gfail * NS; LEX: iteration gfail is left open
     if (tile == 0 && threadIdx.x == 0) {
       R.status[0] = 2;
-      R.status[1] = gfail * NS;
+      R.status[1] = LEX ? gfail : gfail * NS;
     }
     return;
   }
@@ -515,13 +694,13 @@ ResPlan res_plan(int nx, int lo, int hi, int max_tiles) {
   return rp;
 }
 
-void res_launch(int case_id, const Geo& g, const Coef& c, const double* pin, double* pout, const double* f,
+void res_launch(int case_id, bool lex, const Geo& g, const Coef& c, const double* pin, double* pout, const double* f,
                 const ResCtl& R, const ResPlan& rp, int flags, hipStream_t st) {
   const int n = rp.ctiles * rp.rtiles;
-  if (n <= 0 || case_id != CAVITY) return;
+  if (n <= 0 || case_id != CAVITY || rp.rpw != 8) return;
   const dim3 grid(n), block(rp.waves * 64);
-  if (rp.rpw != 8) return;
-  poisson_resident_kernel<8><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
+  if (lex) poisson_resident_kernel<8, true><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
+  else poisson_resident_kernel<8, false><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
 }
 
 }  // namespace cfd

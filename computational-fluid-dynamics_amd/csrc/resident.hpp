@@ -75,6 +75,10 @@ struct ResCtl {
   const double* tol;    // [0] tolerance, [1] initial residual, [2] max|f| (tol_kernel)
   int K;                // sweeps to run (the cap, or the replayed count)
   int check_every;      // the reference tests every iteration (1)
+  // the reference's order (LEX): exceedance bits, 8 shards of bwords words;
+  // iteration k is bit k + koff (koff covers the cells that have not started)
+  unsigned long long* bits;
+  int bwords, koff;
 };
 
 // Tiling of a strip's owned rows [lo, hi) into at most max_tiles tiles, or
@@ -86,7 +90,10 @@ inline size_t res_state_words(int tiles, int K) {
   const size_t n = (size_t)tiles + (size_t)K + 1 + 8;
   return (n + 3) / 4 * 4;
 }
-void res_launch(int case_id, const Geo& g, const Coef& c, const double* pin, double* pout, const double* f,
+void res_launch(int case_id, bool lex, const Geo& g, const Coef& c, const double* pin, double* pout, const double* f,
                 const ResCtl& R, const ResPlan& rp, int flags, hipStream_t st);
+// LEX exceedance-bit words per shard for K iterations on an nx x ny grid, and the bit offset
+inline int res_lex_koff(int nx, int ny) { return (nx + ny) / 2 + 192; }
+inline int res_lex_words(int nx, int ny, int K) { return (res_lex_koff(nx, ny) + K + 256) / 64 + 2; }
 
 }  // namespace cfd

@@ -176,12 +176,15 @@ class Solver {
   double* res_x[2] = {nullptr, nullptr};
   unsigned* res_state = nullptr;
   size_t res_state_n = 0;
+  // (the reference order too: resident.hip's LEX kernel, sampled exceedance
+  // bits instead of the proof; the reference-sized grids keep smlex.hip)
+  unsigned long long* res_bits = nullptr;
+  size_t res_bits_n = 0;
   void plan_resident() {
     res_on = false;
     rplan = ResPlan{};
-    if (!res_knob || P.ordering != CFD_ORDER_RB || S.size() != 1 || comm || P.case_id != CFD_CAVITY || thermal ||
-        !proof_enabled || !(C.proof_k > 0.0))
-      return;
+    if (!res_knob || S.size() != 1 || comm || P.case_id != CFD_CAVITY || thermal) return;
+    if (P.ordering == CFD_ORDER_RB && (!proof_enabled || !(C.proof_k > 0.0))) return;
     const Geo& g = S[0].g;
     rplan = res_plan(P.nx, g.wj0, g.wj1 + 1, n_cu);
     res_on = rplan.ctiles > 0;
@@ -501,6 +504,9 @@ class Solver {
     if (res_state) (void)hipFree(res_state);
     res_state = nullptr;
     res_state_n = 0;
+    if (res_bits) (void)hipFree(res_bits);
+    res_bits = nullptr;
+    res_bits_n = 0;
     lexbits_words = 0;
     if (stop) (void)hipFree(stop);
     stop = nullptr;
@@ -1490,6 +1496,11 @@ class Solver {
       solve_smlex(out);
       return;
     }
+    if (res_on && P.ordering == CFD_ORDER_LEX) {
+      T.sor_kernel = CFD_SOR_RESIDENT;
+      if (!solve_resident_lex(out)) solve_lexw(out);  // an iteration no sample settles: the exact path
+      return;
+    }
     if (use_lexw()) {
       T.sor_kernel = CFD_SOR_LEXW;
       solve_lexw(out);
@@ -1553,7 +1564,7 @@ class Solver {
     R.check_every = std::max(1, P.check_every);
     HIPC(hipMemsetAsync(res_state, 0, words * sizeof(unsigned), st));
     HIPC(hipEventRecord(ev_a, st));
-    res_launch(CAVITY, s.g, C, pin, pout, s.b[B_F], R, rplan, 0, st);
+    res_launch(CAVITY, false, s.g, C, pin, pout, s.b[B_F], R, rplan, 0, st);
     check_launch("poisson (resident)");
     HIPC(hipEventRecord(ev_b, st));
     HIPC(hipMemcpyAsync(h_stat, R.status, 3 * sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1590,7 +1601,7 @@ class Solver {
       HIPC(hipMemsetAsync(res_state, 0, words * sizeof(unsigned), st));
       R.K = k0;
       HIPC(hipEventRecord(ev_a, st));
-      res_launch(CAVITY, s.g, C, pin, pout, s.b[B_F], R, rplan, RES_REPLAY, st);
+      res_launch(CAVITY, false, s.g, C, pin, pout, s.b[B_F], R, rplan, RES_REPLAY, st);
       check_launch("poisson (resident replay)");
       HIPC(hipEventRecord(ev_b, st));
       HIPC(hipMemcpyAsync(h_stat, R.status, 3 * sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1601,6 +1612,91 @@ class Solver {
       if (h_stat[2]) throw Error(CFD_E_STATE, "resident SOR replay: a tile's wait timed out");
     }
     return false;
+  }
+
+  // The reference's order as one resident launch (resident.hip, LEX): every
+  // cell's iterations in the skewed half-sweep order, the stop rule from
+  // sampled residuals. Returns false (nothing changed but the tolerance) when
+  // an iteration before the cap has no sampled exceedance: it may be the
+  // reference's stop, which only the exact evaluation settles (solve_lexw).
+  bool solve_resident_lex(cfd_step_info* out) {
+    Strip& s = S[0];
+    const int base = pcur & 1;
+    const size_t fbytes = (size_t)s.g.nrows * pitch * sizeof(double);
+    double* pin = s.b[pbuf(base)];
+    double* pout = s.b[pbuf(base ^ 1)];
+    HIPC(hipMemsetAsync(pin, 0, fbytes, st));  // cavity-01.cpp:610-611: each solve starts from a zero field
+    solve_tolerance();
+    if (!res_x[0])
+      for (auto*& x : res_x) {
+        HIPC(hipMalloc(&x, fbytes));
+        HIPC(hipMemsetAsync(x, 0, fbytes, st));
+      }
+    const int ntiles = rplan.ctiles * rplan.rtiles, K = P.max_iters;
+    const size_t words = res_state_words(ntiles, K);
+    if (words > res_state_n) {
+      if (res_state) HIPC(hipFree(res_state));
+      res_state = nullptr;
+      HIPC(hipMalloc(&res_state, words * sizeof(unsigned)));
+      res_state_n = words;
+    }
+    const int bwords = res_lex_words(P.nx, P.ny, K);
+    const size_t bn = (size_t)8 * bwords;
+    if (bn > res_bits_n) {
+      if (res_bits) HIPC(hipFree(res_bits));
+      res_bits = nullptr;
+      HIPC(hipMalloc(&res_bits, bn * sizeof(unsigned long long)));
+      res_bits_n = bn;
+    }
+    ResCtl R{};
+    R.xa = res_x[0];
+    R.xb = res_x[1];
+    R.flags = res_state;
+    R.proven = R.flags + ntiles;
+    R.status = reinterpret_cast<int*>(R.proven + K + 1);
+    R.tol = tolv;
+    R.K = K;
+    R.check_every = std::max(1, P.check_every);
+    R.bits = res_bits;
+    R.bwords = bwords;
+    R.koff = res_lex_koff(P.nx, P.ny);
+    HIPC(hipMemsetAsync(res_state, 0, words * sizeof(unsigned), st));
+    HIPC(hipMemsetAsync(res_bits, 0, bn * sizeof(unsigned long long), st));
+    HIPC(hipEventRecord(ev_a, st));
+    res_launch(CAVITY, true, s.g, C, pin, pout, s.b[B_F], R, rplan, 0, st);
+    check_launch("poisson (resident, reference order)");
+    HIPC(hipEventRecord(ev_b, st));
+    HIPC(hipMemcpyAsync(h_stat, R.status, 3 * sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    const int code = h_stat[0], timeout = h_stat[2];
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
+    T.poisson_ms += ms;
+    T.poisson_launches += 1;
+    if (timeout) throw Error(CFD_E_STATE, "resident SOR solve: a tile's wait timed out (tiles not co-resident?)");
+    if (code == 2) {
+      ++T.proof_fallbacks;
+      return false;
+    }
+    if (code != 0 && code != 1) throw Error(CFD_E_STATE, "resident SOR solve: bad status");
+    const int iters = code == 0 ? K : 0;
+    double res;
+    if (iters == 0) {
+      double t2[2];
+      HIPC(hipMemcpy(t2, tolv, sizeof t2, hipMemcpyDeviceToHost));
+      res = t2[1];
+      pcur = base;
+    } else {
+      pcur = base ^ 1;
+      res = final_residual(pbuf(pcur));  // the final field's (cavity-01.cpp:659-677)
+    }
+    T.poisson_sweeps += iters;
+    T.poisson_cell_updates += (long long)P.nx * P.ny * iters;
+    if (out) {
+      out->sor_iterations = iters;
+      out->residual = res;
+    }
+    return true;
   }
 
   // The red-black solve as a sequence of launches (march or LDS tiles). k0 > 0:

@@ -18,13 +18,15 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+LEXW = {"resident": 0}  # the multi-block march (the cavity's resident launch has its own tests: test_gpu_resident.py)
+
 import cfd_amd as C  # noqa: E402
 import oracle as O  # noqa: E402
 from test_gpu_parity import assert_bits, ofield  # noqa: E402
 
 
 def solve_both(cp, f, strips=1, spl=0):
-    g = C.CavitySolver(cp, ordering="lex", small_solve="off", n_strips=strips, sweeps_per_launch=spl)
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off", n_strips=strips, sweeps_per_launch=spl, tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     g.set_field("src", f)
     o.field("src")[...] = f
@@ -67,7 +69,7 @@ def test_converging_solve_stops_at_reference_iteration(spl):
     converges in a few hundred sweeps; the stop is detected up to (nx+ny)/2
     iterations late and replayed to exactly the reference's count."""
     cp = C.reference_defaults("cavity")
-    g = C.CavitySolver(cp, ordering="lex", small_solve="off", sweeps_per_launch=spl)
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off", sweeps_per_launch=spl, tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
     g.computeTentativeVelocities()
@@ -88,7 +90,7 @@ def test_whole_steps_bitexact(case):
         cp, steps = C.reference_defaults("cavity"), 12
     else:  # BASELINE configs[0]
         cp, steps = C.make_params("cavity", re=100.0, nx=128, ny=128, dt=1e-3), 8
-    g = C.CavitySolver(cp, ordering="lex", small_solve="off")
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off", tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
     for k in range(steps):
@@ -100,7 +102,7 @@ def test_whole_steps_bitexact(case):
 def test_cavity_1024_step_bitexact_capped():
     """BASELINE configs[1] size: whole timesteps in the reference's order."""
     cp = C.make_params("cavity", re=1000.0, nx=1024, ny=1024, max_iters=150)
-    g = C.CavitySolver(cp, ordering="lex", small_solve="off")
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off", tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
     for k in range(2):
@@ -114,7 +116,7 @@ def test_cavity_1024_steady_launches_bitexact():
     the steady-state launches (every cell active, poisson_lexw_kernel<*, 4,
     false, *>) run and the step is bit for bit the reference loop's."""
     cp = C.make_params("cavity", re=1000.0, nx=1024, ny=1024, max_iters=1100)
-    g = C.CavitySolver(cp, ordering="lex", small_solve="off")
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off", tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
     assert g.step() == o.step()
@@ -127,7 +129,7 @@ def test_cavity_1024_steady_launches_bitexact():
 def test_cavity_4096_step_bitexact_capped(spl):
     """The bench size: one whole timestep in the reference's order (capped)."""
     cp = C.make_params("cavity", re=1000.0, nx=4096, ny=4096, max_iters=24)
-    g = C.CavitySolver(cp, ordering="lex", small_solve="off", sweeps_per_launch=spl)
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off", sweeps_per_launch=spl, tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     g.applyBoundaryConditions()
     assert g.step() == o.step()
@@ -170,7 +172,7 @@ def test_sampled_rows_open_iterations_exact(seed):
     cp = C.make_params("cavity", nx=90, ny=70, max_iters=3000)
     cp.tol_factor = 1e-6
     f = sparse_source(cp, seed)
-    g = C.CavitySolver(cp, ordering="lex", small_solve="off")
+    g = C.CavitySolver(cp, ordering="lex", small_solve="off", tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     for rep in range(2):
         g.set_field("src", f)

@@ -152,3 +152,90 @@ def test_resident_not_planned_beyond_one_tile_per_cu():
     cp = params(2048, 2048, max_iters=8)
     _, _, tm = run(cp, 1)
     assert _lib.SOR_KERNEL[tm.sor_kernel] != "resident"
+
+
+# ---- the reference's own order (resident.hip LEX): the one-device default ----
+
+def run_lex(cp, steps, resident=True, **kw):
+    """steps whole steps; the timing covers steps 2.. (the first solve from
+    rest has exceedances only at the lid's corners for its first iterations,
+    cells the sampler skips: it may take the exact path)."""
+    g = C.CavitySolver(cp, ordering="lex", device=0, small_solve="off", tuning={"resident": 1 if resident else 0}, **kw)
+    g.applyBoundaryConditions()
+    hist = [g.step()]
+    g.reset_timing()
+    hist += [g.step() for _ in range(steps - 1)]
+    out = {n: g.field(n).copy() for n in FIELDS}
+    tm = g.timing()
+    g.close()
+    return hist, out, tm
+
+
+@pytest.mark.parametrize("nx,ny,steps,cap", [
+    (300, 200, 3, 600), (333, 257, 3, 401), (1024, 64, 3, 600), (113, 130, 3, 500), (110, 110, 3, 300),
+    (222, 96, 3, 403), (500, 300, 3, 1001), (100, 400, 3, 700),
+])
+def test_resident_lex_equals_lexw(nx, ny, steps, cap):
+    """Capped solves in the reference's order: the resident launch (ramps
+    masked, residuals sampled) against the multi-launch march lexw.hpp, which
+    is bit-exact vs the reference loop (tests/test_gpu_lexw.py)."""
+    cp = params(nx, ny, max_iters=cap)
+    hr, fr, tr = run_lex(cp, steps)
+    hw, fw, tw = run_lex(cp, steps, resident=False)
+    assert _lib.SOR_KERNEL[tr.sor_kernel] == "resident"
+    assert _lib.SOR_KERNEL[tw.sor_kernel] == "lexw"
+    assert hr == hw
+    for n in FIELDS:
+        assert_bits(fr[n], fw[n], f"lex {nx}x{ny} {n}")
+    assert tr.proof_fallbacks == 0 and tr.poisson_launches == steps - 1
+
+
+@pytest.mark.parametrize("cap,tol", [(57, None), (5000, 1e-3), (5000, 1e-2)])
+def test_resident_lex_vs_reference_order_oracle(cap, tol):
+    """solverPressurePoisson from one random source in the reference's order
+    (ORC_LEX = the reference loop, pinned against the reference binary):
+    capped, and converging (the stop iteration has no sampled exceedance: the
+    exact path takes over) - iteration count, residual and field bit for bit."""
+    cp = params(160, 100, max_iters=cap, tol=tol)
+    rng = np.random.default_rng(11)
+    f = rng.standard_normal((cp.ny + 2, cp.nx + 2))
+    g = C.CavitySolver(cp, ordering="lex", device=0, small_solve="off", tuning={"resident": 1})
+    o = O.Oracle(cp, ordering=O.LEX)
+    g.set_field("src", f)
+    o.field("src")[...] = f
+    res_g = g.solverPressurePoisson()
+    res_o = o.poisson()
+    tm = g.timing()
+    assert _lib.SOR_KERNEL[tm.sor_kernel] == "resident"
+    assert res_g == res_o
+    if tol is not None:
+        assert res_o[0] < cap and tm.proof_fallbacks >= 1
+    assert_bits(g.field("p"), o.field("p"), f"lex p after {res_o[0]} iterations")
+    g.close()
+
+
+def test_resident_lex_reference_run_vs_oracle():
+    """The reference's own 63^2 run (every solve converges) forced onto the
+    resident path (small_solve off): each solve falls back to the exact
+    path; whole steps bit for bit with the reference loop."""
+    cp = C.reference_defaults("cavity")
+    g = C.CavitySolver(cp, ordering="lex", device=0, small_solve="off", tuning={"resident": 1})
+    o = O.Oracle(cp, ordering=O.LEX)
+    for _ in range(3):
+        assert g.step() == o.step()
+    assert_bits(g.field("p"), o.field("p"), "p")
+    assert_bits(g.field("u"), o.field("u")[:, : cp.nx + 1], "u")
+    g.close()
+
+
+def test_resident_lex_baseline_1024_capped():
+    """BASELINE configs[1] (1024^2, cap 10000) in the reference's order: one
+    whole step per launch equals lexw.hpp bit for bit."""
+    cp = C.make_params("cavity", nx=1024, ny=1024)
+    hr, fr, tr = run_lex(cp, 2)
+    hw, fw, _ = run_lex(cp, 2, resident=False)
+    assert _lib.SOR_KERNEL[tr.sor_kernel] == "resident"
+    assert hr == hw and hr[1][0] == cp.max_iters
+    for n in FIELDS:
+        assert_bits(fr[n], fw[n], f"lex 1024^2 {n}")
+    assert tr.poisson_launches == 1 and tr.proof_fallbacks == 0

@@ -118,7 +118,7 @@ def test_smlex_equals_multiblock_march(case, steps):
     same run: the same iteration counts, residuals and fields, bit for bit."""
     cp = C.reference_defaults(case)
     a = C.solver_for(cp, ordering="lex")
-    b = C.solver_for(cp, ordering="lex", small_solve="off")
+    b = C.solver_for(cp, ordering="lex", small_solve="off", tuning={"resident": 0})
     if case == "cavity":
         a.applyBoundaryConditions()
         b.applyBoundaryConditions()
@@ -167,11 +167,12 @@ def test_maxc_variants_caps_around_checkpoints_bitexact(case, nx, ny, maxc):
         assert _lib.SOR_KERNEL[g.timing().sor_kernel] == "smlex"
 
 
-@pytest.mark.parametrize("nx,ny,kernel", [(110, 88, "smlex"), (140, 69, "lexw")])
+@pytest.mark.parametrize("nx,ny,kernel", [(110, 88, "smlex"), (140, 69, "resident")])
 def test_lds_limit_boundary(nx, ny, kernel):
     """smlex_fits past 4096 cells: p and the source both in LDS, 2 (nx+2)(ny+2)
     <= SMLEX_CELLS = 20160. (nx+2)(ny+2) = 10080 fits, 10082 does not; the
-    grid that does not fit runs the multi-block march, bit for bit the same."""
+    grid that does not fit runs the resident launch (the cavity; the open
+    cases the multi-block march), bit for bit the same."""
     assert (nx + 2) * (ny + 2) == (10080 if kernel == "smlex" else 10082)
     cp = C.make_params("cavity", nx=nx, ny=ny)
     g, _ = run_pair(cp, 2)
@@ -181,8 +182,13 @@ def test_lds_limit_boundary(nx, ny, kernel):
 def test_large_grid_keeps_multiblock_march():
     """Past the LDS (grids over 4096 cells: p and the source in LDS,
     2 (nx+2)(ny+2) <= SMLEX_CELLS = 20160; up to 4096 cells: (nx+2)(ny+2) <=
-    20160) the reference order runs the multi-block march."""
+    20160) the reference order runs the resident launch (the cavity, where one
+    tile per CU covers the grid) or the multi-block march."""
     g = C.solver_for(C.make_params("cavity", nx=128, ny=128), ordering="lex")
+    g.applyBoundaryConditions()
+    g.step()
+    assert _lib.SOR_KERNEL[g.timing().sor_kernel] == "resident"
+    g = C.solver_for(C.make_params("cavity", nx=128, ny=128), ordering="lex", tuning={"resident": 0})
     g.applyBoundaryConditions()
     g.step()
     assert _lib.SOR_KERNEL[g.timing().sor_kernel] == "lexw"
