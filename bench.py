@@ -43,6 +43,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "computational-fluid-dynamics_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_VALU_PEAK_TF = 78.6  # MI355X fp64 vector spec: half the 157.3 TF fp32 vector rate (MI355X_MICROARCH.md)
+FLOPS_PER_UPDATE = 8.0  # the cavity's SOR update: 3 adds, h^2 f, f subtraction, 2 products, 1 add
 BYTES_PER_CELL = 24.0  # SOR launch: read p_in + read f + write p_out, fp64
 METRIC = "Poisson MLUPS + steps/sec, cavity 4096² @1/2/4/8 GPU; % HBM roofline"
 WORKLOAD = {"cavity": "lid-driven cavity", "channel": "channel flow", "backwards_step": "backwards-facing step",
@@ -486,6 +488,20 @@ def run(args, rank: int, world: int, local_rank: int, comm, group, loopback: boo
                 "effective_sweep_frac": round(effective / HBM_PEAK_GBS, 4),
             },
         }
+        if sor_kernel == "resident":
+            # the register-resident whole-solve launch (resident.hpp): p and f*h^2
+            # stay in VGPRs, HBM carries only the tiles' 8-cell edge bands - the
+            # bound is the fp64 VALU work and the group hand-offs, not HBM
+            tflops = FLOPS_PER_UPDATE * updates / elapsed / 1e12
+            line["roofline"] = {
+                "bound": "valu", "achieved": round(tflops, 3), "peak": FP64_VALU_PEAK_TF, "unit": "TFLOP/s",
+                "frac": round(tflops / FP64_VALU_PEAK_TF, 4), "traffic": None,
+                "traffic_source": "none: register-resident solve (no per-sweep HBM stream)",
+                "kernel": f"poisson_resident_kernel<8,{'lex' if args.ordering == 'lex' else 'rb'}> "
+                          "(whole solve in one launch)",
+                "avg_launch_us": round(avg_launch_ms * 1e3, 2), "sweeps_per_launch": round(sweeps_per_launch, 4),
+                "us_per_sweep": round(avg_launch_ms * 1e3 / max(sweeps_per_launch, 1), 4),
+            }
         if loopback:
             line["config"]["loopback_ranks_on_one_gpu"] = world
         if not args.no_cpu_baseline and world == 1:  # the CPU leg is timed at N=1 only
