@@ -33,6 +33,10 @@ struct ResLane {
   double omt_a, omt_b;  // the same in the top row (its north neighbour is the lid's ghost: nc one less)
   double omm_a, omm_b;  // 1 - omega; 1 at ghost / outside columns
   double pa, pb;        // 1.0: a proving cell (owned, 1 < i < nx) of a wave whose rows all prove, else 0.0
+  // channel: slot a is the left ghost column (copy E, window two half-sweeps
+  // late: ush = 2), slot a / b the right ghost column (0)
+  bool lg_a, rg_a, rg_b;
+  int ush_a;
 };
 
 // sor_update<CAVITY> (cavity-01.cpp:643-654) as pc * omm + om * sum in every
@@ -75,7 +79,7 @@ struct LexHalf {
 };
 
 template <int RPW, int COL, bool GEN, bool MASK, bool LEX, int Q0, int NQ>
-__device__ __forceinline__ void res_half_block(const ResLane& L, double2 (&p)[RPW], const double2 (&fh)[RPW],
+__device__ __forceinline__ void res_half_block(const ResLane& L, double2 (&p)[RPW], const double2* fh,
                                                const double2& Sx, const double2& Nx, unsigned fzm, unsigned tpm,
                                                double& dmx, const LexHalf& lh, bool& ex) {
   double pc[NQ], pw[NQ], pe[NQ], sum[NQ], ns[NQ], nv[NQ];
@@ -162,19 +166,135 @@ __device__ __forceinline__ void res_half_block(const ResLane& L, double2 (&p)[RP
   }
 }
 
+// the open cases' source in LDS (their p alone fills the registers of 14-row
+// waves): planes of slot a / slot b values, [region row][lane] (conflict-free
+// 8-B reads; the plane offset fits the reads' immediate offset)
+template <int RPW>
+__host__ __device__ constexpr int res_fplane() { return RES_MAXW * RPW * 64; }
+template <int RPW>
+constexpr size_t res_flds_bytes() { return 2 * (size_t)res_fplane<RPW>() * sizeof(double); }
+
+// ---- channel (channel-01.cpp:652-668, 531-541, 672-681) ----
+//
+// The anisotropic update (sor_update<CHANNEL>: the divide correctly rounded,
+// device.hpp div_denom) in every cell, then the ghost rules of the reference's
+// refresh after each sweep, as cells of their own colour in the skew
+// (lexw.hpp "open cases"): the top ghost row copies its south neighbour and
+// the right ghost column is 0, at their own skew time; the bottom ghost row
+// copies its north neighbour and the left ghost column its east one, two
+// half-sweeps late (the neighbour's previous iteration). Corner ghosts are
+// never read: they and the cells outside the grid run the plain update
+// (bounded, never stored: the corners' initial values are restored at the
+// end). GEN: waves holding a ghost row (per-row fix-ups); EDGE: tiles holding a
+// ghost column (per-lane selects).
+template <int RPW, int COL, bool GEN, bool EDGE, bool MASK, bool LEX, int Q0, int NQ>
+__device__ __forceinline__ void res_half_open(const Coef& c, const ResLane& L, double2 (&p)[RPW], const double* fl,
+                                              const double2& Sx, const double2& Nx, unsigned bgm, unsigned tgm,
+                                              const LexHalf& lh, bool& ex) {
+  double pc[NQ], pw[NQ], pe[NQ], pn[NQ], ps[NQ], nv[NQ];
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) {
+    const int q = Q0 + k;
+    const double2 S = (q == 0) ? Sx : p[q - 1];
+    const double2 N = (q == RPW - 1) ? Nx : p[q + 1];
+    if ((q & 1) == COL) {
+      pc[k] = p[q].x;
+      pw[k] = dpp_from_left(p[q].y);
+      pe[k] = p[q].y;
+      pn[k] = N.x;
+      ps[k] = S.x;
+    } else {
+      pc[k] = p[q].y;
+      pw[k] = p[q].x;
+      pe[k] = dpp_from_right(p[q].x);
+      pn[k] = N.y;
+      ps[k] = S.y;
+    }
+  }
+  const double idx2 = c.idx2, idy2 = c.idy2, omm = c.one_m_omega, om = c.omega;
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) {
+    const int q = Q0 + k;
+    const double fc = fl[((q & 1) == COL ? 0 : res_fplane<RPW>()) + q * 64];
+    const double sum = idx2 * (pe[k] + pw[k]) + idy2 * (pn[k] + ps[k]);
+    nv[k] = omm * pc[k] + om * div_denom(c, sum - fc);
+  }
+  if constexpr (GEN) {  // ghost rows (row-uniform)
+    asm volatile("" : "+s"(bgm), "+s"(tgm));
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int q = Q0 + k;
+      if ((bgm >> q) & 1u) nv[k] = pn[k];
+      if ((tgm >> q) & 1u) nv[k] = ps[k];
+    }
+  }
+  if constexpr (EDGE) {  // ghost columns (lane constants: column 0 is always slot a)
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const bool A = ((Q0 + k) & 1) == COL;
+      if (A) nv[k] = L.lg_a ? pe[k] : nv[k];
+      nv[k] = (A ? L.rg_a : L.rg_b) ? 0.0 : nv[k];
+    }
+  }
+  if constexpr (MASK) {  // the skew's windows (the left / bottom ghosts two half-sweeps late)
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+      const int q = Q0 + k;
+      const bool A = (q & 1) == COL;
+      int u = lh.u0 - q - (A ? L.ush_a : 1);
+      if (GEN && ((bgm >> q) & 1u)) u -= 2;
+      nv[k] = ((unsigned)u <= lh.span) ? nv[k] : pc[k];
+    }
+  }
+  if constexpr (LEX && Q0 <= RES_QS - 1 && Q0 + NQ >= RES_QS + 2) {
+    // sampled residual (channel-01.cpp:672-681) of the other colour's cell of
+    // row RES_QS (2 <= i <= nx-1, 2 <= j <= ny-1: no ghost neighbour)
+    constexpr int kq = RES_QS - Q0;
+    double cv, W, E, fc, mult;
+    if constexpr (COL == 1) {
+      cv = p[RES_QS].y;
+      W = pc[kq];
+      E = dpp_from_right(nv[kq]);
+      fc = lh.fs.y;
+      mult = L.pb;
+    } else {
+      cv = p[RES_QS].x;
+      W = dpp_from_left(pc[kq]);
+      E = nv[kq];
+      fc = lh.fs.x;
+      mult = L.pa;
+    }
+    const double S = pc[kq - 1], N = nv[kq + 1];
+    const double lap = (E - 2.0 * cv + W) * idx2 + (N - 2.0 * cv + S) * idy2;
+    ex = ex || (fabs(lap - fc) > lh.tol && mult != 0.0 && (unsigned)(lh.ks - 1) <= lh.kspan);
+  }
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) {
+    if (((Q0 + k) & 1) == COL) p[Q0 + k].x = nv[k];
+    else p[Q0 + k].y = nv[k];
+  }
+}
+
 // rows in scheduling blocks of RES_BLK (16-row waves: bounded live temporaries)
 #ifndef CFD_RES_BLK
 #define CFD_RES_BLK 8
 #endif
-template <int RPW, int COL, bool GEN, bool MASK, bool LEX, int Q0 = 0>
-__device__ __forceinline__ void res_half(const ResLane& L, double2 (&p)[RPW], const double2 (&fh)[RPW],
-                                         const double2& Sx, const double2& Nx, unsigned fzm, unsigned tpm,
-                                         double& dmx, const LexHalf& lh, bool& ex) {
-  constexpr int NQ = (RPW - Q0) < CFD_RES_BLK ? (RPW - Q0) : CFD_RES_BLK;
-  res_half_block<RPW, COL, GEN, MASK, LEX, Q0, NQ>(L, p, fh, Sx, Nx, fzm, tpm, dmx, lh, ex);
+#ifndef CFD_RES_BLK_OPEN
+#define CFD_RES_BLK_OPEN 7
+#endif
+template <int CASE, int RPW, int COL, bool GEN, bool EDGE, bool MASK, bool LEX, int Q0 = 0>
+__device__ __forceinline__ void res_half(const Coef& c, const ResLane& L, double2 (&p)[RPW], const double2* fh,
+                                         const double* fl, const double2& Sx, const double2& Nx, unsigned fzm,
+                                         unsigned tpm, double& dmx, const LexHalf& lh, bool& ex) {
+  // (larger waves: smaller blocks; the first block holds the sampled rows RES_QS -+ 1)
+  constexpr int BLK = RPW > 8 ? CFD_RES_BLK_OPEN : CFD_RES_BLK;
+  static_assert(BLK >= RES_QS + 2, "the sampled row and its neighbours in the first block");
+  constexpr int NQ = (RPW - Q0) < BLK ? (RPW - Q0) : BLK;
+  if constexpr (CASE == CAVITY) res_half_block<RPW, COL, GEN, MASK, LEX, Q0, NQ>(L, p, fh, Sx, Nx, fzm, tpm, dmx, lh, ex);
+  else res_half_open<RPW, COL, GEN, EDGE, MASK, LEX, Q0, NQ>(c, L, p, fl, Sx, Nx, fzm, tpm, lh, ex);
   if constexpr (Q0 + NQ < RPW) {
     __builtin_amdgcn_sched_barrier(0);
-    res_half<RPW, COL, GEN, MASK, LEX, Q0 + NQ>(L, p, fh, Sx, Nx, fzm, tpm, dmx, lh, ex);
+    res_half<CASE, RPW, COL, GEN, EDGE, MASK, LEX, Q0 + NQ>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx, lh, ex);
   }
 }
 
@@ -226,7 +346,7 @@ __device__ unsigned long long res_stamp_buf[256 * RES_MAXW * RES_STAMP_SEGS];
 
 // One launch = the whole solve (or, red-black, its replay to a known count:
 // RES_REPLAY). LEX: the reference's order.
-template <int RPW, bool LEX>
+template <int CASE, int RPW, bool LEX>
 __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo g, Coef c, const double* __restrict__ pin,
                                                                              double* __restrict__ pout,
                                                                              const double* __restrict__ f, ResCtl R,
@@ -236,6 +356,7 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   __shared__ double red[RES_MAXW][NS + 1];   // red-black: per wave max |p' - p| per sweep, max |p| of the input
   __shared__ int dec;                         // 0 go on, 1 exit (fallback / stop), 2 exit (timeout)
   __shared__ int gdec;                        // red-black: the group a fallback starts at; LEX: the open iteration
+  extern __shared__ double res_fl[];          // (the open cases) the source, res_fplane planes
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int NW = rp.waves;
@@ -263,7 +384,9 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   auto offs = [&](int j) { return ((unsigned)(j - rlo) * P + (unsigned)gxc) * 8u; };
 
   // row classes of this wave (wave-uniform): owned rows, halo rows read at each
-  // group start, frozen rows (ghost rows, rows outside the grid), the top row
+  // group start; cavity: frozen rows (ghost rows, rows outside the grid), the
+  // top row; channel: the bottom (fzm) and top (tpm) ghost rows
+  constexpr bool OPEN = CASE != CAVITY;
   unsigned ownm = 0, haloh = 0, fzm = 0, tpm = 0, rowm = 0;
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
@@ -273,8 +396,8 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     if (r < RR) rowm |= 1u << q;  // region rows (the rest: past the halo, never loaded)
     // region rows read from the neighbours at each group start (grid rows only)
     if (r < RR && !own && j >= 0 && j <= ny + 1) haloh |= 1u << q;
-    if (j <= 0 || j >= ny + 1) fzm |= 1u << q;
-    if (j == ny) tpm |= 1u << q;
+    if (OPEN ? j == 0 : (j <= 0 || j >= ny + 1)) fzm |= 1u << q;
+    if (OPEN ? j == ny + 1 : j == ny) tpm |= 1u << q;
   }
   ownm = __builtin_amdgcn_readfirstlane(ownm);
   haloh = __builtin_amdgcn_readfirstlane(haloh);
@@ -282,7 +405,10 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   tpm = __builtin_amdgcn_readfirstlane(tpm);
   rowm = __builtin_amdgcn_readfirstlane(rowm);
   const bool gen = (fzm | tpm) != 0u;                       // (wave-uniform) the fix-up path
-  const bool proves = !gen && ownm == (1u << RPW) - 1u;     // every row owned and in 1 .. ny - 1
+  // cavity: every row owned and in 1 .. ny - 1 (the proof's cells; the sampled
+  // row's cells); channel: the sampled row owned and in 2 .. ny - 1
+  const bool proves = OPEN ? (((ownm >> RES_QS) & 1u) && jb + RES_QS >= 2 && jb + RES_QS <= ny - 1)
+                           : (!gen && ownm == (1u << RPW) - 1u);
   // lane constants
   const bool own_pair = gx >= x0 && gx < x1;
   ResLane L;
@@ -297,7 +423,13 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     };
     col(gx, L.om_a, L.omt_a, L.omm_a, L.pa);
     col(gx + 1, L.om_b, L.omt_b, L.omm_b, L.pb);
+    L.lg_a = gx == 0;
+    L.rg_a = gx == nx + 1;
+    L.rg_b = gx + 1 == nx + 1;
+    L.ush_a = gx == 0 ? 2 : 0;
   }
+  // channel: a tile whose region holds a ghost column (tile-uniform)
+  const bool edge = OPEN && (c0 <= 0 || c0 + 127 >= nx + 1);
   const bool col_in = gx >= 0 && gx <= nx + 1;      // a grid column pair (its halo cells are published)
   const bool halo_lane = col_in && !own_pair;       // owned rows: this lane's pair belongs to a neighbour
   const bool band_lane = own_pair && (gx < x0 + H || gx >= x1 - H);  // owned pair in the left / right band
@@ -305,7 +437,8 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   // the region from p_in (rows / columns clamped to stored memory: clamped
   // cells lie outside the grid, are never updated and never stored), the
   // source as f * h^2 (LEX: the sampled row's source itself too)
-  double2 p[RPW], fh[RPW];
+  double2 p[RPW], fh[OPEN ? 1 : RPW];
+  double* const fl = res_fl + (w * RPW) * 64 + lane;
   LexHalf lh{};
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
@@ -313,7 +446,12 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     const size_t o = (size_t)(jc - rlo) * (size_t)g.pitch + (size_t)gxc;
     p[q] = *reinterpret_cast<const double2*>(pin + o);
     const double2 F = *reinterpret_cast<const double2*>(f + o);
-    fh[q] = make_double2(F.x * c.h2, F.y * c.h2);
+    if constexpr (OPEN) {
+      fl[q * 64] = F.x;
+      fl[res_fplane<RPW>() + q * 64] = F.y;
+    } else {
+      fh[q] = make_double2(F.x * c.h2, F.y * c.h2);
+    }
     if (LEX && q == RES_QS) lh.fs = F;
   }
   const double tol = R.tol[0];
@@ -329,15 +467,21 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   const int K = R.K;
   // groups: red-black NS sweeps each; LEX: NS half-sweep pairs of the skewed
   // solve, half-sweeps H = 2 .. nx + ny + 2(K - 1) (cell (ny, nx)'s K-th update)
-  const int G = LEX ? (nx + ny + 2 * K - 3 + 2 * NS - 1) / (2 * NS) : res_groups(K);
+  // (the open cases: the top ghost's K-th copy one half-sweep after cell (ny, nx))
+  const int Hlast = nx + ny + 2 * (K - 1) + (OPEN ? 1 : 0);
+  const int G = LEX ? (Hlast - 1 + 2 * NS - 1) / (2 * NS) : res_groups(K);
   lh.span = 2u * (unsigned)(K - 1);
   lh.kspan = (unsigned)(K - 2);
   lh.tol = tol;
   lh.idx2 = c.idx2;
   const int js = jb + RES_QS;  // (LEX) this wave's sampled grid row
-  // LEX: the cells of the region that can change (grid interior): their i + j range
-  const int smin = max(gy0, 1) + max(c0, 1);
-  const int smax = min(gy0 + RR - 1, ny) + min(c0 + 127, nx);
+  // LEX: the cells of the region that can change (cavity: the grid interior;
+  // channel: ghosts too, the left / bottom ones two half-sweeps late): their
+  // i + j range
+  const int GL = OPEN ? 0 : 1;
+  const int smin = max(gy0, GL) + max(c0, GL);
+  const int smax = min(gy0 + RR - 1, ny + 1 - GL) + min(c0 + 127, nx + 1 - GL);
+  const int lag2 = OPEN ? 2 : 0;
   const __amdgpu_buffer_rsrc_t xr[2] = {
       __builtin_amdgcn_make_buffer_rsrc(R.xa, 0, (int)((unsigned)g.nrows * P * 8u), 0x00020000),
       __builtin_amdgcn_make_buffer_rsrc(R.xb, 0, (int)((unsigned)g.nrows * P * 8u), 0x00020000)};
@@ -487,13 +631,14 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     int act = 2;
     if constexpr (LEX) {
       const int He = Hg + 2 * NS - 1;
-      act = (He < smin || Hg - smax > (int)lh.span) ? 0 : (Hg - smax >= 0 && He - smin <= (int)lh.span) ? 2 : 1;
+      act = (He < smin || Hg - smax > (int)lh.span + lag2) ? 0
+            : (Hg - smax >= lag2 && He - smin <= (int)lh.span) ? 2 : 1;
     }
     if (act != 0) exchange();
     if (w == 0 && !replay && !LEX && gi > 0) publish_proofs(gi - 1);  // (red[] of group gi - 1: before the barrier)
     RES_STAMP(2);
     auto sweeps = [&](auto gen_c, auto mask_c) {
-      constexpr bool GEN = decltype(gen_c)::value;
+      constexpr bool GEN = decltype(gen_c)::value;  // (channel: ghost rows or ghost columns)
       constexpr bool MASK = decltype(mask_c)::value;
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
@@ -504,20 +649,21 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
             lh.u0 = Hg + 2 * s - gx - jb;
             lh.ks = (Hg + 2 * s - 1 - gx - js) / 2 + 1;
           }
-          res_half<RPW, 0, GEN, MASK, LEX>(L, p, fh, Sx, Nx, fzm, tpm, dmx[s], lh, ex);
+          res_half<CASE, RPW, 0, GEN, GEN, MASK, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx[s], lh, ex);
           exchange();
           if constexpr (LEX) lh.u0 += 1;
-          res_half<RPW, 1, GEN, MASK, LEX>(L, p, fh, Sx, Nx, fzm, tpm, dmx[s], lh, ex);
+          res_half<CASE, RPW, 1, GEN, GEN, MASK, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx[s], lh, ex);
           if (s + 1 < nsw) exchange();
           if constexpr (LEX) exm |= ex ? (1ull << s) : 0ull;
         }
       }
     };
+    const bool genw = gen || edge;  // (channel: ghost rows in the wave or ghost columns in the tile)
     if (LEX && act == 1) {
-      if (gen) sweeps(std::true_type{}, std::true_type{});
+      if (genw) sweeps(std::true_type{}, std::true_type{});
       else sweeps(std::false_type{}, std::true_type{});
     } else if (act != 0) {
-      if (gen) sweeps(std::true_type{}, std::false_type{});
+      if (genw) sweeps(std::true_type{}, std::false_type{});
       else sweeps(std::false_type{}, std::false_type{});
     }
     RES_STAMP(3);
@@ -653,12 +799,20 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     }
     return;
   }
-  // the final field: owned cells -> p_out
+  // the final field: owned cells -> p_out (channel: the corner ghosts, which the
+  // reference never writes, keep their initial values)
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     const int j = jb + q;
-    if (((ownm >> q) & 1u) && own_pair)
-      *reinterpret_cast<double2*>(pout + (size_t)(j - rlo) * (size_t)g.pitch + (size_t)gx) = p[q];
+    if (((ownm >> q) & 1u) && own_pair) {
+      double2 v = p[q];
+      if (OPEN && (j == 0 || j == ny + 1)) {
+        const double2 v0 = *reinterpret_cast<const double2*>(pin + (size_t)(j - rlo) * (size_t)g.pitch + (size_t)gx);
+        if (gx == 0 || gx == nx + 1) v.x = v0.x;
+        if (gx + 1 == nx + 1) v.y = v0.y;
+      }
+      *reinterpret_cast<double2*>(pout + (size_t)(j - rlo) * (size_t)g.pitch + (size_t)gx) = v;
+    }
   }
   if (!replay && tile == 0 && threadIdx.x == 0) {
     R.status[0] = 0;
@@ -675,7 +829,7 @@ extern "C" int cfd_res_stamps(unsigned long long* out, int n) {
 }
 #endif
 
-ResPlan res_plan(int nx, int lo, int hi, int max_tiles) {
+ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open_lex) {
   ResPlan rp{};
   rp.lo = lo;
   rp.hi = hi;
@@ -688,7 +842,9 @@ ResPlan res_plan(int nx, int lo, int hi, int max_tiles) {
   rp.th = std::max(RES_HALO, (rp.th + 1) / 2 * 2);  // even (region row parity), at least one halo deep
   rp.rtiles = (rows + rp.th - 1) / rp.th;
   const int rr = rp.th + 2 * RES_HALO;
-  rp.rpw = rr <= 8 * RES_MAXW ? 8 : 0;  // (16 rows per wave spill: not planned)
+  // 8 rows per wave; the channel's reference order also RES_RPW_OPEN (its lean
+  // lane constants leave room: 4096x512's 102-row regions)
+  rp.rpw = rr <= 8 * RES_MAXW ? 8 : (open_lex && rr <= RES_RPW_OPEN * RES_MAXW) ? RES_RPW_OPEN : 0;
   if (rp.rpw == 0) return ResPlan{};  // a tile's region exceeds the register budget
   rp.waves = (rr + rp.rpw - 1) / rp.rpw;
   return rp;
@@ -697,10 +853,24 @@ ResPlan res_plan(int nx, int lo, int hi, int max_tiles) {
 void res_launch(int case_id, bool lex, const Geo& g, const Coef& c, const double* pin, double* pout, const double* f,
                 const ResCtl& R, const ResPlan& rp, int flags, hipStream_t st) {
   const int n = rp.ctiles * rp.rtiles;
-  if (n <= 0 || case_id != CAVITY || rp.rpw != 8) return;
+  if (n <= 0) return;
   const dim3 grid(n), block(rp.waves * 64);
-  if (lex) poisson_resident_kernel<8, true><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
-  else poisson_resident_kernel<8, false><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
+  if (case_id == CAVITY && rp.rpw == 8) {
+    if (lex) poisson_resident_kernel<CAVITY, 8, true><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
+    else poisson_resident_kernel<CAVITY, 8, false><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
+  } else if (case_id == CHANNEL && lex) {
+    // (the source in dynamic LDS: past the static 64 KB, an attribute per kernel)
+    auto go = [&](auto kern, size_t lds) {
+      static bool set = false;
+      if (!set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        set = true;
+      }
+      kern<<<grid, block, lds, st>>>(g, c, pin, pout, f, R, rp, flags);
+    };
+    if (rp.rpw == 8) go(poisson_resident_kernel<CHANNEL, 8, true>, res_flds_bytes<8>());
+    else if (rp.rpw == RES_RPW_OPEN) go(poisson_resident_kernel<CHANNEL, RES_RPW_OPEN, true>, res_flds_bytes<RES_RPW_OPEN>());
+  }
 }
 
 }  // namespace cfd

@@ -183,10 +183,13 @@ class Solver {
   void plan_resident() {
     res_on = false;
     rplan = ResPlan{};
-    if (!res_knob || S.size() != 1 || comm || P.case_id != CFD_CAVITY || thermal) return;
+    if (!res_knob || S.size() != 1 || comm || thermal) return;
+    // the cavity in both orders; the channel in the reference's order
+    const bool open_lex = P.case_id == CFD_CHANNEL && P.ordering == CFD_ORDER_LEX;
+    if (P.case_id != CFD_CAVITY && !open_lex) return;
     if (P.ordering == CFD_ORDER_RB && (!proof_enabled || !(C.proof_k > 0.0))) return;
     const Geo& g = S[0].g;
-    rplan = res_plan(P.nx, g.wj0, g.wj1 + 1, n_cu);
+    rplan = res_plan(P.nx, g.wj0, g.wj1 + 1, n_cu, open_lex);
     res_on = rplan.ctiles > 0;
   }
   struct LaunchRec {
@@ -1625,7 +1628,10 @@ class Solver {
     const size_t fbytes = (size_t)s.g.nrows * pitch * sizeof(double);
     double* pin = s.b[pbuf(base)];
     double* pout = s.b[pbuf(base ^ 1)];
-    HIPC(hipMemsetAsync(pin, 0, fbytes, st));  // cavity-01.cpp:610-611: each solve starts from a zero field
+    // the cavity starts each solve from a zero field (cavity-01.cpp:610-611);
+    // the channel from the previous pressure (channel-01.cpp:636), left intact in
+    // p_in for the exact path
+    if (P.case_id == CFD_CAVITY) HIPC(hipMemsetAsync(pin, 0, fbytes, st));
     solve_tolerance();
     if (!res_x[0])
       for (auto*& x : res_x) {
@@ -1663,7 +1669,7 @@ class Solver {
     HIPC(hipMemsetAsync(res_state, 0, words * sizeof(unsigned), st));
     HIPC(hipMemsetAsync(res_bits, 0, bn * sizeof(unsigned long long), st));
     HIPC(hipEventRecord(ev_a, st));
-    res_launch(CAVITY, true, s.g, C, pin, pout, s.b[B_F], R, rplan, 0, st);
+    res_launch(P.case_id == CFD_CHANNEL ? CHANNEL : CAVITY, true, s.g, C, pin, pout, s.b[B_F], R, rplan, 0, st);
     check_launch("poisson (resident, reference order)");
     HIPC(hipEventRecord(ev_b, st));
     HIPC(hipMemcpyAsync(h_stat, R.status, 3 * sizeof(int), hipMemcpyDeviceToHost, st));

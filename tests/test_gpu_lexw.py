@@ -18,7 +18,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-LEXW = {"resident": 0}  # the multi-block march (the cavity's resident launch has its own tests: test_gpu_resident.py)
+LEXW = {"resident": 0}  # the multi-block march (the resident launch has its own tests: test_gpu_resident.py)
 
 import cfd_amd as C  # noqa: E402
 import oracle as O  # noqa: E402
@@ -196,7 +196,7 @@ def random_field(cp, seed, scale=1.0):
 def solve_channel(cp, f, p0, strips=1):
     """One solverPressurePoisson from a given source and initial pressure
     (ghosts included: the reference's first sweep reads them as stored)."""
-    g = C.ChannelSolver(cp, ordering="lex", small_solve="off", n_strips=strips)
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off", n_strips=strips, tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     g.set_field("src", f)
     g.set_field("p", p0)
@@ -228,7 +228,7 @@ def test_channel_converging_solve_bitexact():
     the sampled rows leave the last iterations open and the exact check / the
     continuation must land on the reference's count."""
     cp = C.reference_defaults("channel")
-    g = C.ChannelSolver(cp, ordering="lex", small_solve="off")
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off", tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     o.velocity_bc(False)
     for s in (g, ):
@@ -253,7 +253,7 @@ def test_channel_whole_steps_bitexact(case):
         cp, steps = C.reference_defaults("channel"), 12
     else:
         cp, steps = C.make_params("channel", re=1000.0, nx=384, ny=64, max_iters=200), 3
-    g = C.ChannelSolver(cp, ordering="lex", small_solve="off")
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off", tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     o.velocity_bc(False)
     for k in range(steps):
@@ -266,7 +266,7 @@ def test_channel_4096x512_step_bitexact_capped():
     """BASELINE configs[2] (channel Re=1000, 4096x512): whole timesteps in the
     reference's order, capped, bit for bit."""
     cp = C.make_params("channel", re=1000.0, nx=4096, ny=512, max_iters=30)
-    g = C.ChannelSolver(cp, ordering="lex", small_solve="off")
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off", tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     o.velocity_bc(False)
     for k in range(2):
@@ -279,7 +279,7 @@ def test_channel_4096x512_steady_launches_bitexact():
     """BASELINE configs[2] with the cap past the ramps (K = 2320 > (nx+ny)/2):
     steady-state launches run, bit for bit the reference loop's step."""
     cp = C.make_params("channel", re=1000.0, nx=4096, ny=512, max_iters=2320)
-    g = C.ChannelSolver(cp, ordering="lex", small_solve="off")
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off", tuning=LEXW)
     o = O.Oracle(cp, ordering=O.LEX)
     o.velocity_bc(False)
     assert g.step() == o.step()

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 import cfd_amd as C  # noqa: E402
 import oracle as O  # noqa: E402
 from cfd_amd import _lib  # noqa: E402
-from test_gpu_parity import assert_bits  # noqa: E402
+from test_gpu_parity import assert_bits, ofield  # noqa: E402
 
 FIELDS = ("p", "u", "v")
 RES_TW = 112  # owned columns per tile (resident.hpp)
@@ -239,3 +239,101 @@ def test_resident_lex_baseline_1024_capped():
     for n in FIELDS:
         assert_bits(fr[n], fw[n], f"lex 1024^2 {n}")
     assert tr.poisson_launches == 1 and tr.proof_fallbacks == 0
+
+
+# ---- the channel (configs[2]) in the reference's order: resident.hip res_half_open ----
+
+RES = {"resident": 1}
+
+
+def channel_solve(cp, f, p0, resident=True):
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off", tuning={"resident": 1 if resident else 0})
+    g.set_field("src", f)
+    g.set_field("p", p0)
+    r = g.solverPressurePoisson()
+    out = g.field("p").copy()
+    tm = g.timing()
+    g.close()
+    return r, out, tm
+
+
+@pytest.mark.parametrize("nx,ny,K", [(93, 31, 37), (300, 130, 25), (257, 64, 113), (224, 40, 17), (225, 41, 18),
+                                     (110, 120, 60), (222, 300, 41), (500, 200, 301), (1000, 60, 200)])
+def test_resident_channel_lex_vs_reference_order_oracle(nx, ny, K):
+    """Capped channel solves from an arbitrary pressure (ghosts and corners
+    included: the first sweep reads the ghosts as stored; the corners are never
+    written) on the resident launch: the ghost refreshes in the skew (left /
+    bottom two half-sweeps late), the outlet's zero, outlet ghost in either
+    slot and on tile edges (nx + 2 = 224 / 225 / 226 / 112 ...), several row tiles."""
+    cp = C.make_params("channel", nx=nx, ny=ny, max_iters=K)
+    rng = np.random.default_rng(nx + ny)
+    f = rng.standard_normal((ny + 2, nx + 2)) * 10.0
+    p0 = rng.standard_normal((ny + 2, nx + 2))
+    r, p, tm = channel_solve(cp, f, p0)
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.field("src")[...] = f
+    o.field("p")[...] = p0
+    ro = o.poisson()
+    assert _lib.SOR_KERNEL[tm.sor_kernel] == "resident"
+    assert r == ro and ro[0] == K
+    assert_bits(p, o.field("p"), f"channel resident {nx}x{ny} K={K}")
+    assert tm.proof_fallbacks == 0 and tm.poisson_launches == 1
+
+
+def test_resident_channel_lex_equals_lexw_converging():
+    """Converging channel solves (a 240x80 channel's first steps: each solve
+    stops before the cap): the resident launch leaves the stop open, the exact
+    path (lexw.hpp) takes over from the untouched input - the same counts,
+    residuals and fields as lexw alone."""
+    cp = C.make_params("channel", nx=240, ny=80, max_iters=20000)
+    cp.tol_factor = 1e-3  # (stops at 7915, 11347, 2117: the reference loop restated)
+    out = []
+    for r in (1, 0):
+        g = C.ChannelSolver(cp, ordering="lex", small_solve="off", tuning={"resident": r})
+        hist = [g.step() for _ in range(3)]
+        out.append((hist, g.field("p").copy(), g.field("u").copy(), g.timing()))
+        g.close()
+    (h1, p1, u1, t1), (h2, p2, u2, t2) = out
+    assert _lib.SOR_KERNEL[t1.sor_kernel] == "resident" and _lib.SOR_KERNEL[t2.sor_kernel] == "lexw"
+    assert h1 == h2 and all(k < cp.max_iters for k, _ in h1)
+    assert t1.proof_fallbacks >= 1
+    assert_bits(p1, p2, "channel converging p")
+    assert_bits(u1, u2, "channel converging u")
+
+
+@pytest.mark.parametrize("case", ["reference", "wide"])
+def test_resident_channel_whole_steps_vs_oracle(case):
+    """Whole channel steps (reference 93x31: every solve converges; 384x64
+    capped) with the resident launch, against the reference loop restated."""
+    if case == "reference":
+        cp, steps = C.reference_defaults("channel"), 6
+    else:
+        cp, steps = C.make_params("channel", re=1000.0, nx=384, ny=64, max_iters=200), 3
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off", tuning=RES)
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.velocity_bc(False)
+    for k in range(steps):
+        assert g.step() == o.step(), k
+    assert _lib.SOR_KERNEL[g.timing().sor_kernel] == "resident"
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"channel resident {case} {name}")
+    g.close()
+
+
+@pytest.mark.parametrize("K", [30, 2320])
+def test_resident_channel_4096x512_vs_oracle(K):
+    """BASELINE configs[2] (channel Re=1000, 4096x512: 37 x 6 tiles of 14-row
+    waves): a whole step, capped inside the ramps (30) and past them (2320),
+    one launch, bit for bit the reference loop's step."""
+    cp = C.make_params("channel", re=1000.0, nx=4096, ny=512, max_iters=K)
+    g = C.ChannelSolver(cp, ordering="lex", small_solve="off", tuning=RES)
+    o = O.Oracle(cp, ordering=O.LEX)
+    o.velocity_bc(False)
+    assert g.step() == o.step()
+    tm = g.timing()
+    assert _lib.SOR_KERNEL[tm.sor_kernel] == "resident"
+    if tm.proof_fallbacks == 0:  # (a first step from rest may have no sampled exceedance early on)
+        assert tm.poisson_launches == 1
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"channel 4096x512 K={K} {name}")
+    g.close()
