@@ -847,7 +847,7 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   } else {
     const int ne = (pl.ctiles >= 2) ? 2 : 1;
     const int nbe = pl.nbe0 + pl.nbe1, nbi = pl.nb0 + pl.nb1;
-    int band, th, nb0;
+    int band, th, nb0, part = -1;
     if (tile < ne * nbe) {
       ctile = (tile < nbe) ? 0 : pl.ctiles - 1;
       band = tile % nbe;
@@ -856,15 +856,30 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     } else {
       const int t = tile - ne * nbe;
       const int nci = pl.ctiles - ne;
-      if (t >= nci * nbi) return;
-      ctile = 1 + t % nci;
-      band = t / nci;
+      if (t < nci * nbi) {
+        ctile = 1 + t % nci;
+        band = t / nci;
+        // (the step's split bands: part 0 here, the others below)
+        if (ctile - pl.xa < pl.xn && ctile >= pl.xa && band - pl.xb < pl.xbn && band >= pl.xb) part = 0;
+      } else {
+        const int u = t - nci * nbi, nx = pl.xn * pl.xbn;
+        if (u >= nx * (pl.xparts - 1)) return;
+        const int v = u % nx;
+        part = 1 + u / nx;
+        ctile = pl.xa + v % pl.xn;
+        band = pl.xb + v / pl.xn;
+      }
       th = pl.th;
       nb0 = pl.nb0;
     }
     const bool r0 = band < nb0;
     y0 = r0 ? pl.lo0 + band * th : pl.lo1 + (band - nb0) * th;
     y1 = min(y0 + th, r0 ? pl.hi0 : pl.hi1);
+    if (part >= 0) {
+      const int len = y1 - y0;
+      y1 = y0 + len * (part + 1) / pl.xparts;
+      y0 = y0 + len * part / pl.xparts;
+    }
   }
   constexpr int TWC = lexw_twc(NS);
   const int c0 = ctile * TWC - CH;

@@ -931,6 +931,11 @@ struct PairPlan {
   // between never change, both buffers hold them), the crossing tiles' nxt
   // bands over [le, hi0) (fluid right of the block). ncx = 0: no such class.
   int nl, ncx, nlf, nle, nlt, nxt, lz, le, lt;
+  // step, reference-order steady launches (lexw.hpp): the crossing column
+  // tiles xa .. xa + xn - 1 march their bands xb .. xb + xbn - 1 (those that
+  // reach the block's edge: the per-cell solid rules, ~1.7x the cycles per
+  // row) as xparts shorter bands, the extra parts' waves after the interior ones
+  int xa, xn, xb, xbn, xparts;
 };
 
 // column tiles banded as boundary tiles (masked march): the first and last,

@@ -68,7 +68,10 @@ struct ResLane {
 // residual of the other colour's cells in the half-sweep after their update -
 // W, S before and E, N after this half-sweep's update, exactly the reference's
 // operands (residual_interior<CAVITY>) - and records an exceedance.
-constexpr int RES_QS = 3;  // the sampled row of a wave (odd: a sweep's two samples share one iteration)
+#ifndef CFD_RES_QS
+#define CFD_RES_QS 3
+#endif
+constexpr int RES_QS = CFD_RES_QS;  // the sampled row of a wave (odd: a sweep's two samples share one iteration)
 struct LexHalf {
   int u0;          // H - gx - jb: cell (row q, slot a) active iff (unsigned)(u0 - q) <= span; slot b: u0 - q - 1
   unsigned span;   // 2 (K - 1)
@@ -190,7 +193,7 @@ constexpr size_t res_flds_bytes() { return 2 * (size_t)res_fplane<RPW>() * sizeo
 template <int RPW, int COL, bool GEN, bool EDGE, bool MASK, bool LEX, int Q0, int NQ>
 __device__ __forceinline__ void res_half_open(const Coef& c, const ResLane& L, double2 (&p)[RPW], const double* fl,
                                               const double2& Sx, const double2& Nx, unsigned bgm, unsigned tgm,
-                                              const LexHalf& lh, bool& ex) {
+                                              double& dmx, bool keep, const LexHalf& lh, bool& ex) {
   double pc[NQ], pw[NQ], pe[NQ], pn[NQ], ps[NQ], nv[NQ];
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
@@ -219,21 +222,23 @@ __device__ __forceinline__ void res_half_open(const Coef& c, const ResLane& L, d
     const double sum = idx2 * (pe[k] + pw[k]) + idy2 * (pn[k] + ps[k]);
     nv[k] = omm * pc[k] + om * div_denom(c, sum - fc);
   }
+  // (red-black: the red ghosts keep the stored values in the solve's first
+  // half-sweep, `keep` - the reference's first sweep reads them as stored)
   if constexpr (GEN) {  // ghost rows (row-uniform)
     asm volatile("" : "+s"(bgm), "+s"(tgm));
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
       const int q = Q0 + k;
-      if ((bgm >> q) & 1u) nv[k] = pn[k];
-      if ((tgm >> q) & 1u) nv[k] = ps[k];
+      if ((bgm >> q) & 1u) nv[k] = keep ? pc[k] : pn[k];
+      if ((tgm >> q) & 1u) nv[k] = keep ? pc[k] : ps[k];
     }
   }
   if constexpr (EDGE) {  // ghost columns (lane constants: column 0 is always slot a)
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
       const bool A = ((Q0 + k) & 1) == COL;
-      if (A) nv[k] = L.lg_a ? pe[k] : nv[k];
-      nv[k] = (A ? L.rg_a : L.rg_b) ? 0.0 : nv[k];
+      if (A) nv[k] = L.lg_a ? (keep ? pc[k] : pe[k]) : nv[k];
+      nv[k] = (A ? L.rg_a : L.rg_b) ? (keep ? pc[k] : 0.0) : nv[k];
     }
   }
   if constexpr (MASK) {  // the skew's windows (the left / bottom ghosts two half-sweeps late)
@@ -267,6 +272,9 @@ __device__ __forceinline__ void res_half_open(const Coef& c, const ResLane& L, d
     const double S = pc[kq - 1], N = nv[kq + 1];
     const double lap = (E - 2.0 * cv + W) * idx2 + (N - 2.0 * cv + S) * idy2;
     ex = ex || (fabs(lap - fc) > lh.tol && mult != 0.0 && (unsigned)(lh.ks - 1) <= lh.kspan);
+  } else if constexpr (!LEX && COL == 1) {  // red-black proof: max |p' - p| of the proving black cells
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) dmx = fmax(dmx, fabs(nv[k] - pc[k]) * ((((Q0 + k) & 1) == COL) ? L.pa : L.pb));
   }
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
@@ -275,9 +283,15 @@ __device__ __forceinline__ void res_half_open(const Coef& c, const ResLane& L, d
   }
 }
 
+#ifndef CFD_RES_RB1
+#define CFD_RES_RB1 1
+#endif
 // rows in scheduling blocks of RES_BLK (16-row waves: bounded live temporaries)
 #ifndef CFD_RES_BLK
 #define CFD_RES_BLK 8
+#endif
+#ifndef CFD_RES_BLK_RB
+#define CFD_RES_BLK_RB 7
 #endif
 #ifndef CFD_RES_BLK_OPEN
 #define CFD_RES_BLK_OPEN 7
@@ -285,16 +299,16 @@ __device__ __forceinline__ void res_half_open(const Coef& c, const ResLane& L, d
 template <int CASE, int RPW, int COL, bool GEN, bool EDGE, bool MASK, bool LEX, int Q0 = 0>
 __device__ __forceinline__ void res_half(const Coef& c, const ResLane& L, double2 (&p)[RPW], const double2* fh,
                                          const double* fl, const double2& Sx, const double2& Nx, unsigned fzm,
-                                         unsigned tpm, double& dmx, const LexHalf& lh, bool& ex) {
+                                         unsigned tpm, double& dmx, bool keep, const LexHalf& lh, bool& ex) {
   // (larger waves: smaller blocks; the first block holds the sampled rows RES_QS -+ 1)
-  constexpr int BLK = RPW > 8 ? CFD_RES_BLK_OPEN : CFD_RES_BLK;
-  static_assert(BLK >= RES_QS + 2, "the sampled row and its neighbours in the first block");
+  constexpr int BLK = RPW > 8 ? (LEX ? CFD_RES_BLK_OPEN : CFD_RES_BLK_RB) : CFD_RES_BLK;
+  static_assert(!LEX || BLK >= RES_QS + 2, "the sampled row and its neighbours in the first block");
   constexpr int NQ = (RPW - Q0) < BLK ? (RPW - Q0) : BLK;
   if constexpr (CASE == CAVITY) res_half_block<RPW, COL, GEN, MASK, LEX, Q0, NQ>(L, p, fh, Sx, Nx, fzm, tpm, dmx, lh, ex);
-  else res_half_open<RPW, COL, GEN, EDGE, MASK, LEX, Q0, NQ>(c, L, p, fl, Sx, Nx, fzm, tpm, lh, ex);
+  else res_half_open<RPW, COL, GEN, EDGE, MASK, LEX, Q0, NQ>(c, L, p, fl, Sx, Nx, fzm, tpm, dmx, keep, lh, ex);
   if constexpr (Q0 + NQ < RPW) {
     __builtin_amdgcn_sched_barrier(0);
-    res_half<CASE, RPW, COL, GEN, EDGE, MASK, LEX, Q0 + NQ>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx, lh, ex);
+    res_half<CASE, RPW, COL, GEN, EDGE, MASK, LEX, Q0 + NQ>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx, keep, lh, ex);
   }
 }
 
@@ -353,7 +367,8 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
                                                                              ResPlan rp, int flags) {
   constexpr int NS = RES_NS, H = RES_HALO, TW = RES_TW;
   __shared__ double2 E[2][RES_MAXW][2][64];  // the waves' first / last rows after each half-sweep (by parity)
-  __shared__ double red[RES_MAXW][NS + 1];   // red-black: per wave max |p' - p| per sweep, max |p| of the input
+  __shared__ double red[2][RES_MAXW][NS + 1];  // red-black: per wave max |p' - p| per sweep, max |p| of the
+                                               // input (group parity: wave 0 reads one while the waves write the other)
   __shared__ int dec;                         // 0 go on, 1 exit (fallback / stop), 2 exit (timeout)
   __shared__ int gdec;                        // red-black: the group a fallback starts at; LEX: the open iteration
   extern __shared__ double res_fl[];          // (the open cases) the source, res_fplane planes
@@ -381,7 +396,10 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   const int rlo = g.row_lo, rhi = g.row_lo + g.nrows - 1;  // stored rows
   const int gxc = min(max(gx, 0), g.pitch - 2);
   const unsigned P = (unsigned)g.pitch;
-  auto offs = [&](int j) { return ((unsigned)(j - rlo) * P + (unsigned)gxc) * 8u; };
+  // (a row's byte offset from a base made opaque per group: the rows' offsets
+  // are recomputed where used instead of hoisted out of the group loop as
+  // 2 x RPW live registers - spilled at 14 rows per wave)
+  auto offs = [&](int j, unsigned base) { return (unsigned)(j - rlo) * P * 8u + base; };
 
   // row classes of this wave (wave-uniform): owned rows, halo rows read at each
   // group start; cavity: frozen rows (ghost rows, rows outside the grid), the
@@ -407,8 +425,10 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   const bool gen = (fzm | tpm) != 0u;                       // (wave-uniform) the fix-up path
   // cavity: every row owned and in 1 .. ny - 1 (the proof's cells; the sampled
   // row's cells); channel: the sampled row owned and in 2 .. ny - 1
-  const bool proves = OPEN ? (((ownm >> RES_QS) & 1u) && jb + RES_QS >= 2 && jb + RES_QS <= ny - 1)
-                           : (!gen && ownm == (1u << RPW) - 1u);
+  // (channel, red-black: every row owned and in 2 .. ny - 1)
+  const bool proves = (OPEN && LEX) ? (((ownm >> RES_QS) & 1u) && jb + RES_QS >= 2 && jb + RES_QS <= ny - 1)
+                      : OPEN ? (ownm == (1u << RPW) - 1u && jb >= 2 && jb + RPW - 1 <= ny - 1)
+                             : (!gen && ownm == (1u << RPW) - 1u);
   // lane constants
   const bool own_pair = gx >= x0 && gx < x1;
   ResLane L;
@@ -525,7 +545,7 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     double dm = 0.0, pv = 0.0;
     if (lane < NS + 1)
       for (int v = 0; v < NW; ++v) {
-        const double x = red[v][lane];
+        const double x = red[gq & 1][v][lane];
         if (lane < NS) dm = fmax(dm, x);
         else pv = fmax(pv, x);
       }
@@ -582,11 +602,13 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (the loads stay after the poll)
       const __amdgpu_buffer_rsrc_t xp = xr[(gi - 1) & 1];
+      unsigned ob = (unsigned)gxc * 8u;
+      asm volatile("" : "+v"(ob));
 #pragma unroll
       for (int q = 0; q < RPW; ++q) {
         const bool hrow = (haloh >> q) & 1u;
         const bool orow = (ownm >> q) & 1u;
-        if ((hrow && col_in) || (orow && halo_lane)) p[q] = ld_sc1(xp, offs(jb + q));
+        if ((hrow && col_in) || (orow && halo_lane)) p[q] = ld_sc1(xp, offs(jb + q, ob));
       }
     }
     pend_g = -1;
@@ -635,11 +657,34 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
             : (Hg - smax >= lag2 && He - smin <= (int)lh.span) ? 2 : 1;
     }
     if (act != 0) exchange();
-    if (w == 0 && !replay && !LEX && gi > 0) publish_proofs(gi - 1);  // (red[] of group gi - 1: before the barrier)
     RES_STAMP(2);
     auto sweeps = [&](auto gen_c, auto mask_c) {
       constexpr bool GEN = decltype(gen_c)::value;  // (channel: ghost rows or ghost columns)
       constexpr bool MASK = decltype(mask_c)::value;
+      if constexpr (OPEN && !LEX) {
+        // (the channel's red-black sweeps as a loop: its short last group's
+        // conditional sweeps, unrolled, need ~160 more registers at 14 rows)
+        double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+        bool ex = false;
+#pragma unroll 1
+        for (int s = 0; s < nsw; ++s) {
+          double dm = 0.0;
+          res_half<CASE, RPW, 0, GEN, GEN, MASK, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dm, gi == 0 && s == 0, lh, ex);
+          exchange();
+          res_half<CASE, RPW, 1, GEN, GEN, MASK, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dm, false, lh, ex);
+          if (s + 1 < nsw) exchange();
+          d0 = s == 0 ? dm : d0;
+          d1 = s == 1 ? dm : d1;
+          d2 = s == 2 ? dm : d2;
+          d3 = s == 3 ? dm : d3;
+        }
+        static_assert(NS == 4, "the loop's per-sweep proof values");
+        dmx[0] = d0;
+        dmx[1] = d1;
+        dmx[2] = d2;
+        dmx[3] = d3;
+        return;
+      }
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         dmx[s] = 0.0;
@@ -649,10 +694,11 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
             lh.u0 = Hg + 2 * s - gx - jb;
             lh.ks = (Hg + 2 * s - 1 - gx - js) / 2 + 1;
           }
-          res_half<CASE, RPW, 0, GEN, GEN, MASK, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx[s], lh, ex);
+          res_half<CASE, RPW, 0, GEN, GEN, MASK, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx[s], !LEX && gi == 0 && s == 0,
+                                                      lh, ex);
           exchange();
           if constexpr (LEX) lh.u0 += 1;
-          res_half<CASE, RPW, 1, GEN, GEN, MASK, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx[s], lh, ex);
+          res_half<CASE, RPW, 1, GEN, GEN, MASK, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx[s], false, lh, ex);
           if (s + 1 < nsw) exchange();
           if constexpr (LEX) exm |= ex ? (1ull << s) : 0ull;
         }
@@ -662,6 +708,8 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     if (LEX && act == 1) {
       if (genw) sweeps(std::true_type{}, std::true_type{});
       else sweeps(std::false_type{}, std::true_type{});
+    } else if (OPEN && !LEX && CFD_RES_RB1) {
+      sweeps(std::true_type{}, std::false_type{});  // (one variant: the fix-ups are no-ops off the ghosts)
     } else if (act != 0) {
       if (genw) sweeps(std::true_type{}, std::false_type{});
       else sweeps(std::false_type{}, std::false_type{});
@@ -694,20 +742,25 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       pm = wave_max(pm);
       if (lane == 0) {
 #pragma unroll
-        for (int s = 0; s < NS; ++s) red[w][s] = dmx[s];
-        red[w][NS] = pm;
+        for (int s = 0; s < NS; ++s) red[gi & 1][w][s] = dmx[s];
+        red[gi & 1][w][NS] = pm;
       }
     }
     {
       const __amdgpu_buffer_rsrc_t xo = xr[gi & 1];
+      unsigned ob = (unsigned)gxc * 8u;
+      asm volatile("" : "+v"(ob));
 #pragma unroll
       for (int q = 0; q < RPW; ++q) {
         const int j = jb + q;
         const bool orow = (ownm >> q) & 1u;
         const bool brow = j < y0 + H || j >= y1 - H;  // (row-uniform) in the bottom / top band
-        if (orow && own_pair && (brow || band_lane)) st_sc1(xo, offs(j), p[q]);
+        if (orow && own_pair && (brow || band_lane)) st_sc1(xo, offs(j, ob), p[q]);
       }
     }
+    // (red-black) the proofs of group gi - 1, published at this group's end, off
+    // the sweeps' register peak; drained before flag gi + 1 like the bands
+    if (w == 0 && !replay && !LEX && gi > 0) publish_proofs(gi - 1);
     if constexpr (LEX) {
       if (w == 0 && pk1 >= pk0) {
         const int ko = lex_first_open(pend, pk0, pk1);
@@ -829,7 +882,27 @@ extern "C" int cfd_res_stamps(unsigned long long* out, int n) {
 }
 #endif
 
-ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open_lex) {
+// the channel's ghost refresh (channel-01.cpp:531-541; corners untouched) of
+// a resident red-black solve's final field: its red ghosts took their last
+// copy one sweep back (resident.hip: ghosts as cells of their own colour)
+__global__ void res_refresh_kernel(Geo g, double* __restrict__ p) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nx = g.nx, ny = g.ny;
+  if (t >= 1 && t <= ny && t >= g.row_lo && t < g.row_lo + g.nrows) {
+    p[at(g, t, 0)] = p[at(g, t, 1)];
+    p[at(g, t, nx + 1)] = 0.0;
+  }
+  if (t >= 1 && t <= nx) {
+    if (g.row_lo <= 0 && g.row_lo + g.nrows > 1) p[at(g, 0, t)] = p[at(g, 1, t)];
+    if (g.row_lo <= ny && g.row_lo + g.nrows > ny + 1) p[at(g, ny + 1, t)] = p[at(g, ny, t)];
+  }
+}
+void res_refresh(const Geo& g, double* p, hipStream_t st) {
+  const int n = std::max(g.nx, g.ny) + 1;
+  res_refresh_kernel<<<(n + 255) / 256, 256, 0, st>>>(g, p);
+}
+
+ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open) {
   ResPlan rp{};
   rp.lo = lo;
   rp.hi = hi;
@@ -842,9 +915,9 @@ ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open_lex) {
   rp.th = std::max(RES_HALO, (rp.th + 1) / 2 * 2);  // even (region row parity), at least one halo deep
   rp.rtiles = (rows + rp.th - 1) / rp.th;
   const int rr = rp.th + 2 * RES_HALO;
-  // 8 rows per wave; the channel's reference order also RES_RPW_OPEN (its lean
-  // lane constants leave room: 4096x512's 102-row regions)
-  rp.rpw = rr <= 8 * RES_MAXW ? 8 : (open_lex && rr <= RES_RPW_OPEN * RES_MAXW) ? RES_RPW_OPEN : 0;
+  // 8 rows per wave; the channel also RES_RPW_OPEN (its source in LDS leaves
+  // room: 4096x512's 102-row regions)
+  rp.rpw = rr <= 8 * RES_MAXW ? 8 : (open && rr <= RES_RPW_OPEN * RES_MAXW) ? RES_RPW_OPEN : 0;
   if (rp.rpw == 0) return ResPlan{};  // a tile's region exceeds the register budget
   rp.waves = (rr + rp.rpw - 1) / rp.rpw;
   return rp;
@@ -858,7 +931,7 @@ void res_launch(int case_id, bool lex, const Geo& g, const Coef& c, const double
   if (case_id == CAVITY && rp.rpw == 8) {
     if (lex) poisson_resident_kernel<CAVITY, 8, true><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
     else poisson_resident_kernel<CAVITY, 8, false><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
-  } else if (case_id == CHANNEL && lex) {
+  } else if (case_id == CHANNEL) {
     // (the source in dynamic LDS: past the static 64 KB, an attribute per kernel)
     auto go = [&](auto kern, size_t lds) {
       static bool set = false;
@@ -868,8 +941,13 @@ void res_launch(int case_id, bool lex, const Geo& g, const Coef& c, const double
       }
       kern<<<grid, block, lds, st>>>(g, c, pin, pout, f, R, rp, flags);
     };
-    if (rp.rpw == 8) go(poisson_resident_kernel<CHANNEL, 8, true>, res_flds_bytes<8>());
-    else if (rp.rpw == RES_RPW_OPEN) go(poisson_resident_kernel<CHANNEL, RES_RPW_OPEN, true>, res_flds_bytes<RES_RPW_OPEN>());
+    if (lex) {
+      if (rp.rpw == 8) go(poisson_resident_kernel<CHANNEL, 8, true>, res_flds_bytes<8>());
+      else if (rp.rpw == RES_RPW_OPEN) go(poisson_resident_kernel<CHANNEL, RES_RPW_OPEN, true>, res_flds_bytes<RES_RPW_OPEN>());
+    } else {
+      if (rp.rpw == 8) go(poisson_resident_kernel<CHANNEL, 8, false>, res_flds_bytes<8>());
+      else if (rp.rpw == RES_RPW_OPEN) go(poisson_resident_kernel<CHANNEL, RES_RPW_OPEN, false>, res_flds_bytes<RES_RPW_OPEN>());
+    }
   }
 }
 

@@ -83,7 +83,9 @@ struct ResCtl {
 
 // Tiling of a strip's owned rows [lo, hi) into at most max_tiles tiles, or
 // ctiles = 0 if the grid does not fit (the solver keeps the per-launch kernels)
-ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open_lex = false);
+ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open = false);
+// the channel's ghost refresh of a final field (red-black resident solve)
+void res_refresh(const Geo& g, double* p, hipStream_t st);
 constexpr int RES_RPW_OPEN = 14;  // rows per wave of the channel's larger tiles (reference order)
 __host__ __device__ inline int res_groups(int K) { return (K + RES_NS - 1) / RES_NS; }
 // unsigned words of flags + proofs + status, rounded to 16 B

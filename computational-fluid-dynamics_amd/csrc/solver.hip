@@ -184,12 +184,12 @@ class Solver {
     res_on = false;
     rplan = ResPlan{};
     if (!res_knob || S.size() != 1 || comm || thermal) return;
-    // the cavity in both orders; the channel in the reference's order
-    const bool open_lex = P.case_id == CFD_CHANNEL && P.ordering == CFD_ORDER_LEX;
-    if (P.case_id != CFD_CAVITY && !open_lex) return;
+    // the cavity and the channel, both orders
+    const bool open = P.case_id == CFD_CHANNEL;
+    if (P.case_id != CFD_CAVITY && !open) return;
     if (P.ordering == CFD_ORDER_RB && (!proof_enabled || !(C.proof_k > 0.0))) return;
     const Geo& g = S[0].g;
-    rplan = res_plan(P.nx, g.wj0, g.wj1 + 1, n_cu, open_lex);
+    rplan = res_plan(P.nx, g.wj0, g.wj1 + 1, n_cu, open);
     res_on = rplan.ctiles > 0;
   }
   struct LaunchRec {
@@ -1026,6 +1026,9 @@ class Solver {
   // the march (lexw.hpp step_presolid_kernel), so that the column tiles left
   // of the step's column end at the block's bottom row and march as a channel
   // below it (flags bit 3; CFD_TUNE_LEXW_LEFT 0: the per-cell masked march)
+#ifndef CFD_LEXW_XSPLIT
+#define CFD_LEXW_XSPLIT 3
+#endif
   bool lexw_left_class() const { return P.case_id == CFD_BACKSTEP && lexw_left; }
   void lexw_presolid() {
     if (!lexw_left_class()) return;
@@ -1096,10 +1099,37 @@ class Solver {
       if (th > pl.th) ntiles = build(th = std::max(pl.th, (rh - rl) / LEXW_RAMP_BANDS + 1));
       if (pl.ctiles > 255 || ntiles >= 65536) throw Error(CFD_E_ARG, "lexicographic ordering: grid too wide");
     }
+    // the step's steady launches: the crossing column tiles' bands that reach
+    // the block's edge as CFD_LEXW_XSPLIT shorter bands (lexw.hpp; they set
+    // the launch's time: profiles/r5/step_8192x512_lex_stamps.json)
+    PairPlan plx = pl;
+    if (steady && P.case_id == CFD_BACKSTEP && CFD_LEXW_XSPLIT > 1 && pl.nb1 == 0 && pl.ctiles >= 3) {
+      const int twc = lexw_twc(ns), ch = lexw_ch(ns), jb = C.inlet_jmax + 1, si = C.step_i;
+      int xa = -1, xn = 0;
+      for (int ct = 1; ct + 1 < pl.ctiles; ++ct) {
+        const int c0 = ct * twc - ch;
+        const bool left = c0 + 127 <= si - 1 && lexw_left_class();
+        if (!left && c0 <= si + 1) {
+          if (xa < 0) xa = ct;
+          xn = ct - xa + 1;
+        }
+      }
+      int xb = -1;
+      for (int b = 0; b < pl.nb0 && xb < 0; ++b)
+        if (std::min(pl.lo0 + (b + 1) * pl.th, pl.hi0) + 4 * ns + 4 >= jb) xb = b;
+      if (xa >= 0 && xb >= 0) {
+        plx.xa = xa;
+        plx.xn = xn;
+        plx.xb = xb;
+        plx.xbn = pl.nb0 - xb;
+        plx.xparts = CFD_LEXW_XSPLIT;
+        ntiles += plx.xn * plx.xbn * (plx.xparts - 1);
+      }
+    }
     if (ntiles == 0) return;
     const dim3 grid((ntiles + 3) / 4);
 #define CFD_LEXW_LAUNCH(CASE, NS, R, SM) \
-  poisson_lexw_kernel<CASE, NS, R, SM><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, pl, fl, rp)
+  poisson_lexw_kernel<CASE, NS, R, SM><<<grid, 256, 0, st>>>(g, C, pin, pout, f, L, H0, K, ka, kb, plx, fl, rp)
     // (sampled residual rows: the 3-sweep kernels, the default; 1 and 2 sweeps evaluate every row)
     if (P.case_id == CFD_BACKSTEP && ns == 3) {  // (strips)
       if (sample) { if (steady) CFD_LEXW_LAUNCH(BACKSTEP, 3, false, true); else CFD_LEXW_LAUNCH(BACKSTEP, 3, true, true); }
@@ -1541,7 +1571,11 @@ class Solver {
     const size_t fbytes = (size_t)s.g.nrows * pitch * sizeof(double);
     double* pin = s.b[pbuf(base)];
     double* pout = s.b[pbuf((base + 1) % nbufs())];
-    HIPC(hipMemsetAsync(pin, 0, fbytes, st));  // cavity-01.cpp:610-611: each solve starts from a zero field
+    // the cavity starts each solve from a zero field (cavity-01.cpp:610-611),
+    // the channel from the previous pressure (channel-01.cpp:636)
+    if (P.case_id == CFD_CAVITY) HIPC(hipMemsetAsync(pin, 0, fbytes, st));
+    const bool open = P.case_id == CFD_CHANNEL;
+    const int cid = open ? CHANNEL : CAVITY;
     solve_tolerance();
     if (!res_x[0])
       for (auto*& x : res_x) {
@@ -1567,8 +1601,9 @@ class Solver {
     R.check_every = std::max(1, P.check_every);
     HIPC(hipMemsetAsync(res_state, 0, words * sizeof(unsigned), st));
     HIPC(hipEventRecord(ev_a, st));
-    res_launch(CAVITY, false, s.g, C, pin, pout, s.b[B_F], R, rplan, 0, st);
+    res_launch(cid, false, s.g, C, pin, pout, s.b[B_F], R, rplan, 0, st);
     check_launch("poisson (resident)");
+    if (open) res_refresh(s.g, pout, st);  // the refresh after the last sweep (its red ghosts)
     HIPC(hipEventRecord(ev_b, st));
     HIPC(hipMemcpyAsync(h_stat, R.status, 3 * sizeof(int), hipMemcpyDeviceToHost, st));
     HIPC(hipStreamSynchronize(st));
@@ -1604,8 +1639,9 @@ class Solver {
       HIPC(hipMemsetAsync(res_state, 0, words * sizeof(unsigned), st));
       R.K = k0;
       HIPC(hipEventRecord(ev_a, st));
-      res_launch(CAVITY, false, s.g, C, pin, pout, s.b[B_F], R, rplan, RES_REPLAY, st);
+      res_launch(cid, false, s.g, C, pin, pout, s.b[B_F], R, rplan, RES_REPLAY, st);
       check_launch("poisson (resident replay)");
+      if (open) res_refresh(s.g, pout, st);
       HIPC(hipEventRecord(ev_b, st));
       HIPC(hipMemcpyAsync(h_stat, R.status, 3 * sizeof(int), hipMemcpyDeviceToHost, st));
       HIPC(hipStreamSynchronize(st));

@@ -337,3 +337,101 @@ def test_resident_channel_4096x512_vs_oracle(K):
     for name in ("u", "v", "p"):
         assert_bits(g.field(name), ofield(o, name, cp), f"channel 4096x512 K={K} {name}")
     g.close()
+
+
+# ---- the channel (configs[2]) in red-black order: ghosts as cells of their colour ----
+
+def channel_rb(cp, f, p0, resident=True):
+    g = C.ChannelSolver(cp, ordering="rb", small_solve="off", tuning={"resident": 1 if resident else 0})
+    g.set_field("src", f)
+    g.set_field("p", p0)
+    r = g.solverPressurePoisson()
+    out = g.field("p").copy()
+    tm = g.timing()
+    g.close()
+    return r, out, tm
+
+
+@pytest.mark.parametrize("nx,ny,K", [(240, 120, 57), (93, 31, 37), (300, 130, 25), (224, 40, 17), (225, 41, 18),
+                                     (110, 120, 60), (222, 300, 41), (500, 200, 301), (1000, 60, 203), (240, 120, 1),
+                                     (240, 120, 4), (240, 120, 5)])
+def test_resident_channel_rb_vs_red_black_oracle(nx, ny, K):
+    """Capped channel solves from an arbitrary pressure (ghosts and corners
+    included) on the resident launch: the red ghosts keep their stored values
+    in the first half-sweep and take the last refresh after the launch, the
+    outlet's zero, ghosts on tile edges, short last groups (K mod 4) - against
+    the oracle's red-black restatement, bit for bit."""
+    cp = C.make_params("channel", nx=nx, ny=ny, max_iters=K)
+    rng = np.random.default_rng(nx * 7 + ny)
+    f = rng.standard_normal((ny + 2, nx + 2)) * 10.0
+    p0 = rng.standard_normal((ny + 2, nx + 2))
+    r, p, tm = channel_rb(cp, f, p0)
+    o = O.Oracle(cp, ordering=O.RB)
+    o.field("src")[...] = f
+    o.field("p")[...] = p0
+    ro = o.poisson()
+    assert _lib.SOR_KERNEL[tm.sor_kernel] == "resident"
+    assert r == ro and ro[0] == K
+    assert_bits(p, o.field("p"), f"channel rb resident {nx}x{ny} K={K}")
+    if tm.proof_fallbacks == 0:
+        assert tm.poisson_launches == 1
+
+
+def test_resident_channel_rb_converging_equals_march():
+    """Converging channel solves (240x80, loose tolerance, three steps): the
+    proof leaves the stop's group open, the replay and the exact launches
+    finish - the same counts, residuals and fields as the march alone."""
+    cp = C.make_params("channel", nx=240, ny=80, max_iters=20000)
+    cp.tol_factor = 1e-3
+    out = []
+    for r in (1, 0):
+        g = C.ChannelSolver(cp, ordering="rb", small_solve="off", tuning={"resident": r})
+        hist = [g.step() for _ in range(3)]
+        out.append((hist, g.field("p").copy(), g.field("u").copy(), g.timing()))
+        g.close()
+    (h1, p1, u1, t1), (h2, p2, u2, t2) = out
+    assert _lib.SOR_KERNEL[t1.sor_kernel] == "resident" and _lib.SOR_KERNEL[t2.sor_kernel] != "resident"
+    assert h1 == h2 and all(k < cp.max_iters for k, _ in h1)
+    assert t1.proof_fallbacks >= 1
+    assert_bits(p1, p2, "channel rb converging p")
+    assert_bits(u1, u2, "channel rb converging u")
+
+
+@pytest.mark.parametrize("case", ["reference", "wide"])
+def test_resident_channel_rb_whole_steps_vs_oracle(case):
+    """Whole red-black channel steps (reference 93x31: every solve converges;
+    384x64 capped) on the resident launch against the oracle."""
+    if case == "reference":
+        cp, steps = C.reference_defaults("channel"), 6
+    else:
+        cp, steps = C.make_params("channel", re=1000.0, nx=384, ny=64, max_iters=200), 3
+    g = C.ChannelSolver(cp, ordering="rb", small_solve="off", tuning=RES)
+    o = O.Oracle(cp, ordering=O.RB)
+    o.velocity_bc(False)
+    for k in range(steps):
+        assert g.step() == o.step(), k
+    assert _lib.SOR_KERNEL[g.timing().sor_kernel] == "resident"
+    for name in ("u", "v", "p"):
+        assert_bits(g.field(name), ofield(o, name, cp), f"channel rb resident {case} {name}")
+    g.close()
+
+
+def test_resident_channel_rb_4096x512_equals_march():
+    """BASELINE configs[2] (channel Re=1000, 4096x512, cap 10000): two whole
+    red-black steps on the resident launch (14-row waves) equal the march
+    launches bit for bit; the second solve is one launch."""
+    cp = C.make_params("channel", re=1000.0, nx=4096, ny=512)
+    out = []
+    for r in (1, 0):
+        g = C.ChannelSolver(cp, ordering="rb", small_solve="off", tuning={"resident": r})
+        hist = [g.step()]
+        g.reset_timing()
+        hist.append(g.step())
+        out.append((hist, {n: g.field(n).copy() for n in FIELDS}, g.timing()))
+        g.close()
+    (h1, f1, t1), (h2, f2, _) = out
+    assert _lib.SOR_KERNEL[t1.sor_kernel] == "resident"
+    assert h1 == h2 and h1[1][0] == cp.max_iters
+    for n in FIELDS:
+        assert_bits(f1[n], f2[n], f"channel rb 4096x512 {n}")
+    assert t1.poisson_launches == 1 and t1.proof_fallbacks == 0
