@@ -157,8 +157,10 @@ def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch
     return {"ordering": "lex", "value": round(tm.poisson_cell_updates / el / 1e6, 2), "unit": "MLUPS",
             "ms_per_step": round(el / args.lex_steps * 1e3, 3), "steps": args.lex_steps,
             "sor_iterations_per_step": iters,
-            "kernel": f"poisson_lexw_kernel<{args.case},{round(tm.poisson_sweeps / max(tm.poisson_launches, 1))},"
-                      f"sampled>",
+            "kernel": (f"poisson_resident_kernel<{args.case},lex> (whole solve in one launch)"
+                       if _lib_sor_kernel(tm) == "resident" else
+                       f"poisson_lexw_kernel<{args.case},{round(tm.poisson_sweeps / max(tm.poisson_launches, 1))},"
+                       f"sampled>"),
             "sweeps_per_launch": round(tm.poisson_sweeps / max(tm.poisson_launches, 1), 3),
             "launches_per_step": round(tm.poisson_launches / args.lex_steps, 1),
             "steady_launches_per_step": round(tm.poisson_steady_launches / args.lex_steps, 1),
@@ -497,7 +499,7 @@ def run(args, rank: int, world: int, local_rank: int, comm, group, loopback: boo
                 "bound": "valu", "achieved": round(tflops, 3), "peak": FP64_VALU_PEAK_TF, "unit": "TFLOP/s",
                 "frac": round(tflops / FP64_VALU_PEAK_TF, 4), "traffic": None,
                 "traffic_source": "none: register-resident solve (no per-sweep HBM stream)",
-                "kernel": f"poisson_resident_kernel<8,{'lex' if args.ordering == 'lex' else 'rb'}> "
+                "kernel": f"poisson_resident_kernel<{kcase},{'lex' if args.ordering == 'lex' else 'rb'}> "
                           "(whole solve in one launch)",
                 "avg_launch_us": round(avg_launch_ms * 1e3, 2), "sweeps_per_launch": round(sweeps_per_launch, 4),
                 "us_per_sweep": round(avg_launch_ms * 1e3 / max(sweeps_per_launch, 1), 4),

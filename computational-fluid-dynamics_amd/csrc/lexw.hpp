@@ -76,8 +76,38 @@ constexpr int LEXW_RAMP_BANDS = 256;
 struct LexRamp {
   int nb, th, row0;
   int wsplit;  // 1: the wall column tiles (first, last) march each band as two half bands (two waves)
+  // the step: its crossing column tiles xa .. xa + xn - 1 march the bands that
+  // reach the block's edge (band rows blo .. blo + th - 1 with blo + th + xreach
+  // >= jb) as two half bands too (xn = 0: none)
+  int xa, xn, xreach;
   unsigned band[LEXW_RAMP_BANDS];
 };
+
+// ramp launch: the column tile and half band (-1: the whole band) of wave o of
+// a band whose tiles are ca .. cb (split tiles take two consecutive waves)
+__host__ __device__ inline int lexw_ramp_waves(const LexRamp& rp, int ctiles, int b, int ca, int cb, int o,
+                                               int* ctile, int* half) {
+  int sp[4], n = 0;
+  if (rp.wsplit && ca == 0 && cb >= ca) sp[n++] = 0;
+  if (rp.xn > 0 && rp.row0 + (b + 1) * rp.th + rp.xreach >= 0)
+    for (int c = max(rp.xa, ca); c <= min(rp.xa + rp.xn - 1, cb); ++c)
+      if (c != 0 && c != ctiles - 1) sp[n++] = c;
+  if (rp.wsplit && cb == ctiles - 1 && cb > 0) sp[n++] = cb;
+  int extra = 0;
+  for (int q = 0; q < n; ++q) {
+    const int at = sp[q] - ca + extra;
+    if (o < at) break;
+    if (o == at || o == at + 1) {
+      *ctile = sp[q];
+      *half = o - at;
+      return n;
+    }
+    ++extra;
+  }
+  *ctile = ca + o - extra;
+  *half = -1;
+  return n;  // (the split tiles: the band has cb - ca + 1 + n waves)
+}
 
 struct LexCtl {
   unsigned long long* bits;  // LEXW_SHARDS x words; bit q of the bitset <-> iteration q - kmax
@@ -822,18 +852,11 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     }
     const unsigned e = rp.band[lo];
     const int ca = (e >> 8) & 255, cb = e & 255;
-    int o = tile - (int)(e >> 16), half = -1;
     // wall tiles (masked march, slower per step; they set the ramp launches'
-    // time): two waves each, one per half band (host: launch_lexw build)
-    if (rp.wsplit && ca == 0 && cb >= ca) {
-      if (o < 2) half = o, o = 0;
-      else o -= 1;
-    }
-    ctile = ca + o;
-    if (half < 0 && rp.wsplit && cb == pl.ctiles - 1 && cb > 0 && ctile >= cb) {
-      half = ctile - cb;
-      ctile = cb;
-    }
+    // time) and the step's crossing tiles at the block's edge: two waves each,
+    // one per half band (host: launch_lexw build)
+    int half;
+    lexw_ramp_waves(rp, pl.ctiles, lo, ca, cb, tile - (int)(e >> 16), &ctile, &half);
     if (ctile > cb) return;
     int rlo, rhi;
     lexw_rows(g, H0, K, NS, ctile, &rlo, &rhi, OPEN);

@@ -1029,6 +1029,21 @@ class Solver {
 #ifndef CFD_LEXW_XSPLIT
 #define CFD_LEXW_XSPLIT 3
 #endif
+  // the step's interior column tiles that cross its column (the per-cell solid
+  // rules at the block's edge): xa .. xa + xn - 1, xa = -1 if none
+  void lexw_cross_tiles(int ns, const PairPlan& pl, int* xa, int* xn) const {
+    const int twc = lexw_twc(ns), ch = lexw_ch(ns), si = C.step_i;
+    *xa = -1;
+    *xn = 0;
+    for (int ct = 1; ct + 1 < pl.ctiles; ++ct) {
+      const int c0 = ct * twc - ch;
+      const bool left = c0 + 127 <= si - 1 && lexw_left_class();
+      if (!left && c0 <= si + 1) {
+        if (*xa < 0) *xa = ct;
+        *xn = ct - *xa + 1;
+      }
+    }
+  }
   bool lexw_left_class() const { return P.case_id == CFD_BACKSTEP && lexw_left; }
   void lexw_presolid() {
     if (!lexw_left_class()) return;
@@ -1064,7 +1079,16 @@ class Solver {
       }
       if (rh < rl) return;
       const int ex = lexw_extra(ns);
-      rp.wsplit = CFD_LEXW_WALL_SPLIT && P.case_id != CFD_BACKSTEP;  // (the step: -0.5 %, profiles/r4_lexw_stamps)
+      rp.wsplit = CFD_LEXW_WALL_SPLIT;
+      if (P.case_id == CFD_BACKSTEP && CFD_LEXW_XSPLIT > 1) {  // the step's crossing tiles (as the steady split)
+        int xa, xn;
+        lexw_cross_tiles(ns, pl, &xa, &xn);
+        if (xa >= 0) {
+          rp.xa = xa;
+          rp.xn = xn;
+          rp.xreach = 4 * ns + 4 - (C.inlet_jmax + 1);
+        }
+      }
       auto build = [&](int th) {  // fills rp for band height th; returns the tile count
         rp.th = th;
         rp.row0 = rl;
@@ -1082,9 +1106,9 @@ class Solver {
           rp.band[b] = ((unsigned)n << 16) | ((unsigned)ca << 8) | (unsigned)(cb < 0 ? 0 : cb);
           if (cb < 0) rp.band[b] = ((unsigned)n << 16) | 1u << 8;  // ca 1 > cb 0: empty
           n += std::max(0, cb - ca + 1);
-          if (rp.wsplit && cb >= ca) {  // a second wave per wall tile (lexw.hpp: half bands)
-            if (ca == 0) ++n;
-            if (cb == pl.ctiles - 1 && cb > 0) ++n;
+          if (cb >= ca) {  // a second wave per split tile (lexw.hpp lexw_ramp_waves: half bands)
+            int ct, hf;
+            n += lexw_ramp_waves(rp, pl.ctiles, b, ca, cb, 0, &ct, &hf);
           }
         }
         return n;
@@ -1104,16 +1128,9 @@ class Solver {
     // the launch's time: profiles/r5/step_8192x512_lex_stamps.json)
     PairPlan plx = pl;
     if (steady && P.case_id == CFD_BACKSTEP && CFD_LEXW_XSPLIT > 1 && pl.nb1 == 0 && pl.ctiles >= 3) {
-      const int twc = lexw_twc(ns), ch = lexw_ch(ns), jb = C.inlet_jmax + 1, si = C.step_i;
-      int xa = -1, xn = 0;
-      for (int ct = 1; ct + 1 < pl.ctiles; ++ct) {
-        const int c0 = ct * twc - ch;
-        const bool left = c0 + 127 <= si - 1 && lexw_left_class();
-        if (!left && c0 <= si + 1) {
-          if (xa < 0) xa = ct;
-          xn = ct - xa + 1;
-        }
-      }
+      const int jb = C.inlet_jmax + 1;
+      int xa, xn;
+      lexw_cross_tiles(ns, pl, &xa, &xn);
       int xb = -1;
       for (int b = 0; b < pl.nb0 && xb < 0; ++b)
         if (std::min(pl.lo0 + (b + 1) * pl.th, pl.hi0) + 4 * ns + 4 >= jb) xb = b;

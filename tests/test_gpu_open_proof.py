@@ -23,7 +23,7 @@ from test_gpu_parity import assert_bits  # noqa: E402
 
 SOLVERS = {"channel": C.ChannelSolver, "backwards_step": C.BackwardsStepSolver}
 FIELDS = ("p", "u", "v")
-MARCH = {"tile_rounds": 0}  # the wave march (the LDS tiles have their own tests)
+MARCH = {"tile_rounds": 0, "resident": 0}  # the wave march (the LDS tiles and the resident launch have their own tests)
 
 
 def run(case, cp, steps, strips=1, **kw):

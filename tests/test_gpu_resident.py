@@ -398,22 +398,28 @@ def test_resident_channel_rb_converging_equals_march():
 
 
 @pytest.mark.parametrize("case", ["reference", "wide"])
-def test_resident_channel_rb_whole_steps_vs_oracle(case):
+def test_resident_channel_rb_whole_steps_equal_march(case):
     """Whole red-black channel steps (reference 93x31: every solve converges;
-    384x64 capped) on the resident launch against the oracle."""
+    384x64 capped) on the resident launch and on the march launches: counts,
+    residuals and fields bit for bit. (Against the oracle the red-black
+    channel step differs in the source's mean removal - a tree sum here, the
+    sequential sum only in the reference's order: test_gpu_parity.py - so the
+    march, itself pinned to the oracle solve by solve, is the reference.)"""
     if case == "reference":
         cp, steps = C.reference_defaults("channel"), 6
     else:
         cp, steps = C.make_params("channel", re=1000.0, nx=384, ny=64, max_iters=200), 3
-    g = C.ChannelSolver(cp, ordering="rb", small_solve="off", tuning=RES)
-    o = O.Oracle(cp, ordering=O.RB)
-    o.velocity_bc(False)
-    for k in range(steps):
-        assert g.step() == o.step(), k
-    assert _lib.SOR_KERNEL[g.timing().sor_kernel] == "resident"
+    out = []
+    for r in (1, 0):
+        g = C.ChannelSolver(cp, ordering="rb", small_solve="off", tuning={"resident": r})
+        hist = [g.step() for _ in range(steps)]
+        out.append((hist, {n: g.field(n).copy() for n in ("u", "v", "p")}, g.timing()))
+        g.close()
+    (h1, f1, t1), (h2, f2, t2) = out
+    assert _lib.SOR_KERNEL[t1.sor_kernel] == "resident" and _lib.SOR_KERNEL[t2.sor_kernel] != "resident"
+    assert h1 == h2
     for name in ("u", "v", "p"):
-        assert_bits(g.field(name), ofield(o, name, cp), f"channel rb resident {case} {name}")
-    g.close()
+        assert_bits(f1[name], f2[name], f"channel rb resident {case} {name}")
 
 
 def test_resident_channel_rb_4096x512_equals_march():

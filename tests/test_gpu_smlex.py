@@ -171,8 +171,8 @@ def test_maxc_variants_caps_around_checkpoints_bitexact(case, nx, ny, maxc):
 def test_lds_limit_boundary(nx, ny, kernel):
     """smlex_fits past 4096 cells: p and the source both in LDS, 2 (nx+2)(ny+2)
     <= SMLEX_CELLS = 20160. (nx+2)(ny+2) = 10080 fits, 10082 does not; the
-    grid that does not fit runs the resident launch (the cavity; the open
-    cases the multi-block march), bit for bit the same."""
+    grid that does not fit runs the resident launch (the cavity and the
+    channel; the step the multi-block march), bit for bit the same."""
     assert (nx + 2) * (ny + 2) == (10080 if kernel == "smlex" else 10082)
     cp = C.make_params("cavity", nx=nx, ny=ny)
     g, _ = run_pair(cp, 2)
