@@ -18,6 +18,7 @@ rc=$?; echo "bench exit $rc"; cat $D/bench.json; [ $rc -ne 0 ] && { tail -5 $D/b
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/stats -o run --output-format csv -- python3 bench.py $A --steps 1 --warmup 1 > $D/stats.out 2> $D/stats.err
 rc=$?; echo "rocprof exit $rc"; [ $rc -ne 0 ] && { tail -5 $D/stats.err; exit $rc; }
 find $D/stats -name '*kernel_stats.csv' -exec head -4 {} \;
+[ -n "$NO_PMC" ] && exit 0  # (the resident whole-solve launch: no per-sweep HBM stream to count)
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 150 rocprofv3 --pmc $c -d $D/$c -o run --output-format csv -- python3 bench.py $A --steps 1 $W --max-iters ${PMC_ITERS:-400} > $D/$c.out 2> $D/$c.err
   rc=$?; echo "pmc $c exit $rc"; [ $rc -ne 0 ] && { tail -5 $D/$c.err; exit $rc; }
