@@ -72,6 +72,9 @@ struct ResLane {
 #define CFD_RES_QS 3
 #endif
 constexpr int RES_QS = CFD_RES_QS;  // the sampled row of a wave (odd: a sweep's two samples share one iteration)
+#ifndef CFD_RES_OPEN_PROOF_ALL
+#define CFD_RES_OPEN_PROOF_ALL 0
+#endif
 struct LexHalf {
   int u0;          // H - gx - jb: cell (row q, slot a) active iff (unsigned)(u0 - q) <= span; slot b: u0 - q - 1
   unsigned span;   // 2 (K - 1)
@@ -272,9 +275,15 @@ __device__ __forceinline__ void res_half_open(const Coef& c, const ResLane& L, d
     const double S = pc[kq - 1], N = nv[kq + 1];
     const double lap = (E - 2.0 * cv + W) * idx2 + (N - 2.0 * cv + S) * idy2;
     ex = ex || (fabs(lap - fc) > lh.tol && mult != 0.0 && (unsigned)(lh.ks - 1) <= lh.kspan);
-  } else if constexpr (!LEX && COL == 1) {  // red-black proof: max |p' - p| of the proving black cells
+  } else if constexpr (!LEX && COL == 1) {
+    // red-black proof: max |p' - p| of the proving black cells - of one row
+    // per wave (CFD_RES_OPEN_PROOF_ALL 0: any subset of cells proves "the
+    // reference goes on" when one of them does; every row's pc kept for it
+    // spilled the 14-row kernel), or of every row
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) dmx = fmax(dmx, fabs(nv[k] - pc[k]) * ((((Q0 + k) & 1) == COL) ? L.pa : L.pb));
+    for (int k = 0; k < NQ; ++k)
+      if (CFD_RES_OPEN_PROOF_ALL || Q0 + k == RES_QS)
+        dmx = fmax(dmx, fabs(nv[k] - pc[k]) * ((((Q0 + k) & 1) == COL) ? L.pa : L.pb));
   }
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
@@ -283,9 +292,6 @@ __device__ __forceinline__ void res_half_open(const Coef& c, const ResLane& L, d
   }
 }
 
-#ifndef CFD_RES_RB1
-#define CFD_RES_RB1 1
-#endif
 // rows in scheduling blocks of RES_BLK (16-row waves: bounded live temporaries)
 #ifndef CFD_RES_BLK
 #define CFD_RES_BLK 8
@@ -661,17 +667,31 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     auto sweeps = [&](auto gen_c, auto mask_c) {
       constexpr bool GEN = decltype(gen_c)::value;  // (channel: ghost rows or ghost columns)
       constexpr bool MASK = decltype(mask_c)::value;
-      if constexpr (OPEN && !LEX) {
-        // (the channel's red-black sweeps as a loop: its short last group's
-        // conditional sweeps, unrolled, need ~160 more registers at 14 rows)
+      if constexpr (OPEN && !LEX && !MASK) {
+        // (the channel's red-black full groups, unrolled: interior waves run the
+        // lean update, the ghost waves / tiles the fix-ups)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          dmx[s] = 0.0;
+          bool ex = false;
+          res_half<CASE, RPW, 0, GEN, GEN, false, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx[s], GEN && gi == 0 && s == 0,
+                                                       lh, ex);
+          exchange();
+          res_half<CASE, RPW, 1, GEN, GEN, false, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dmx[s], false, lh, ex);
+          if (s + 1 < NS) exchange();
+        }
+        return;
+      } else if constexpr (OPEN && !LEX) {
+        // (MASK here: the short last group, as a loop in the general variant -
+        // its conditional sweeps, unrolled, need ~160 more registers at 14 rows)
         double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
         bool ex = false;
 #pragma unroll 1
         for (int s = 0; s < nsw; ++s) {
           double dm = 0.0;
-          res_half<CASE, RPW, 0, GEN, GEN, MASK, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dm, gi == 0 && s == 0, lh, ex);
+          res_half<CASE, RPW, 0, true, true, false, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dm, gi == 0 && s == 0, lh, ex);
           exchange();
-          res_half<CASE, RPW, 1, GEN, GEN, MASK, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dm, false, lh, ex);
+          res_half<CASE, RPW, 1, true, true, false, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dm, false, lh, ex);
           if (s + 1 < nsw) exchange();
           d0 = s == 0 ? dm : d0;
           d1 = s == 1 ? dm : d1;
@@ -708,8 +728,10 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     if (LEX && act == 1) {
       if (genw) sweeps(std::true_type{}, std::true_type{});
       else sweeps(std::false_type{}, std::true_type{});
-    } else if (OPEN && !LEX && CFD_RES_RB1) {
-      sweeps(std::true_type{}, std::false_type{});  // (one variant: the fix-ups are no-ops off the ghosts)
+    } else if (OPEN && !LEX) {
+      if (nsw < NS) sweeps(std::true_type{}, std::true_type{});  // (the short last group: the general loop)
+      else if (genw) sweeps(std::true_type{}, std::false_type{});
+      else sweeps(std::false_type{}, std::false_type{});
     } else if (act != 0) {
       if (genw) sweeps(std::true_type{}, std::false_type{});
       else sweeps(std::false_type{}, std::false_type{});

@@ -4,7 +4,7 @@ step; per wave the cycles of its neighbour waits, halo loads, first exchange,
 sweeps and group end, summed over the solve; printed per group (mean over the
 tiles' waves, and the slowest wave).
 
-usage: CFD_AMD_LIB=libcfd_amd_rstamps.so python3 scripts/dbg/res_stamps.py nx ny [max_iters]
+usage: CFD_AMD_LIB=libcfd_amd_rstamps.so python3 scripts/dbg/res_stamps.py nx ny [max_iters] [case] [order]
 """
 import ctypes
 import json
@@ -18,9 +18,12 @@ from cfd_amd import _lib  # noqa: E402
 
 nx, ny = int(sys.argv[1]), int(sys.argv[2])
 iters = int(sys.argv[3]) if len(sys.argv) > 3 else 10000
-cp = C.make_params("cavity", nx=nx, ny=ny, max_iters=iters)
-s = C.CavitySolver(cp, device=0, ordering="rb", small_solve="off", tuning={"resident": 1})
-s.applyBoundaryConditions()
+case = sys.argv[4] if len(sys.argv) > 4 else "cavity"
+order = sys.argv[5] if len(sys.argv) > 5 else "rb"
+cp = C.make_params(case, nx=nx, ny=ny, max_iters=iters)
+s = C.solver_for(cp, device=0, ordering=order, small_solve="off", tuning={"resident": 1})
+if case == "cavity":
+    s.applyBoundaryConditions()
 s.step()
 s.reset_timing()
 s.step()
@@ -34,13 +37,16 @@ a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8, 6).astype(np.float64)
 groups = a[:, :, 5]
 used = groups > 0
 names = ["wait", "halo", "first_exchange", "sweeps", "end"]
-out = {"nx": nx, "ny": ny, "iters": iters, "solve_ms": tm.poisson_ms, "launches": tm.poisson_launches,
+out = {"case": case, "order": order, "nx": nx, "ny": ny, "iters": iters, "solve_ms": tm.poisson_ms, "launches": tm.poisson_launches,
        "fallbacks": tm.proof_fallbacks, "waves": int(used.sum()),
        "us_per_sweep": 1000 * tm.poisson_ms / iters}
 for k, nm in enumerate(names):
     per_group = a[:, :, k][used] / groups[used]
     out[nm + "_cyc_per_group_mean"] = round(float(per_group.mean()), 1)
     out[nm + "_cyc_per_group_max"] = round(float(per_group.max()), 1)
+    # per wave index (wave 0 polls; the first / last waves hold the top / bottom halo rows)
+    out[nm + "_by_wave"] = [round(float((a[:, w, k][used[:, w]] / groups[:, w][used[:, w]]).mean()), 1)
+                            if used[:, w].any() else None for w in range(8)]
 tot = sum(a[:, :, k] for k in range(5))[used] / groups[used]
 out["total_cyc_per_group_mean"] = round(float(tot.mean()), 1)
 print(json.dumps(out, indent=1))
