@@ -122,14 +122,17 @@ __device__ __forceinline__ void res_half_block(const ResLane& L, double2 (&p)[RP
     const bool A = ((Q0 + k) & 1) == COL;
     nv[k] = pc[k] * (A ? L.omm_a : L.omm_b) + (A ? L.om_a : L.om_b) * sum[k];
   }
-  if constexpr (GEN) {
+  if constexpr (GEN) {  // (a block without a frozen / top row skips the fix-ups)
     asm volatile("" : "+s"(fzm), "+s"(tpm));
+    constexpr unsigned BM = ((1u << NQ) - 1u) << Q0;
+    if ((fzm | tpm) & BM) {
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-      const int q = Q0 + k;
-      const bool A = (q & 1) == COL;
-      if ((tpm >> q) & 1u) nv[k] = pc[k] * (A ? L.omm_a : L.omm_b) + (A ? L.omt_a : L.omt_b) * sum[k];
-      if ((fzm >> q) & 1u) nv[k] = pc[k];
+      for (int k = 0; k < NQ; ++k) {
+        const int q = Q0 + k;
+        const bool A = (q & 1) == COL;
+        if ((tpm >> q) & 1u) nv[k] = pc[k] * (A ? L.omm_a : L.omm_b) + (A ? L.omt_a : L.omt_b) * sum[k];
+        if ((fzm >> q) & 1u) nv[k] = pc[k];
+      }
     }
   }
   if constexpr (MASK) {  // the reference order's windows (ramps)
@@ -227,13 +230,16 @@ __device__ __forceinline__ void res_half_open(const Coef& c, const ResLane& L, d
   }
   // (red-black: the red ghosts keep the stored values in the solve's first
   // half-sweep, `keep` - the reference's first sweep reads them as stored)
-  if constexpr (GEN) {  // ghost rows (row-uniform)
+  constexpr unsigned BM = ((1u << NQ) - 1u) << Q0;  // this block's rows
+  if constexpr (GEN) {  // ghost rows (row-uniform; a block without one skips the selects)
     asm volatile("" : "+s"(bgm), "+s"(tgm));
+    if ((bgm | tgm) & BM) {
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-      const int q = Q0 + k;
-      if ((bgm >> q) & 1u) nv[k] = keep ? pc[k] : pn[k];
-      if ((tgm >> q) & 1u) nv[k] = keep ? pc[k] : ps[k];
+      for (int k = 0; k < NQ; ++k) {
+        const int q = Q0 + k;
+        if ((bgm >> q) & 1u) nv[k] = keep ? pc[k] : pn[k];
+        if ((tgm >> q) & 1u) nv[k] = keep ? pc[k] : ps[k];
+      }
     }
   }
   if constexpr (EDGE) {  // ghost columns (lane constants: column 0 is always slot a)

@@ -47,6 +47,15 @@ for k, nm in enumerate(names):
     # per wave index (wave 0 polls; the first / last waves hold the top / bottom halo rows)
     out[nm + "_by_wave"] = [round(float((a[:, w, k][used[:, w]] / groups[:, w][used[:, w]]).mean()), 1)
                             if used[:, w].any() else None for w in range(8)]
+# per tile class: the first / last column tiles (ghost columns) vs the others
+ctiles = (nx + 2 + 111) // 112
+tiles = np.arange(256)
+edge = ((tiles % ctiles) == 0) | ((tiles % ctiles) == ctiles - 1)
+for nm, k in (("sweeps", 3), ("wait", 0), ("end", 4)):
+    for cls, sel in (("edge_tiles", edge), ("inner_tiles", ~edge)):
+        u = used & sel[:, None]
+        if u.any():
+            out[f"{nm}_{cls}_mean"] = round(float((a[:, :, k][u] / groups[u]).mean()), 1)
 tot = sum(a[:, :, k] for k in range(5))[used] / groups[used]
 out["total_cyc_per_group_mean"] = round(float(tot.mean()), 1)
 print(json.dumps(out, indent=1))
