@@ -37,6 +37,9 @@ struct ResLane {
   // late: ush = 2), slot a / b the right ghost column (0)
   bool lg_a, rg_a, rg_b;
   int ush_a;
+  // (tile-uniform) the tile holds the left / right ghost column; the right one
+  // sits in slot a (nx + 1 even)
+  bool has_lg, has_rg, rg_in_a;
 };
 
 // sor_update<CAVITY> (cavity-01.cpp:643-654) as pc * omm + om * sum in every
@@ -243,11 +246,24 @@ __device__ __forceinline__ void res_half_open(const Coef& c, const ResLane& L, d
     }
   }
   if constexpr (EDGE) {  // ghost columns (lane constants: column 0 is always slot a)
+    // (a tile holds at most one of them in most grids, and a row's updated
+    // colour holds a ghost cell only in its slot: tile-uniform branches, one
+    // select per row where a ghost is updated)
+    if (L.has_lg) {
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) {
-      const bool A = ((Q0 + k) & 1) == COL;
-      if (A) nv[k] = L.lg_a ? (keep ? pc[k] : pe[k]) : nv[k];
-      nv[k] = (A ? L.rg_a : L.rg_b) ? (keep ? pc[k] : 0.0) : nv[k];
+      for (int k = 0; k < NQ; ++k)
+        if (((Q0 + k) & 1) == COL) nv[k] = L.lg_a ? (keep ? pc[k] : pe[k]) : nv[k];
+    }
+    if (L.has_rg) {
+      if (L.rg_in_a) {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k)
+          if (((Q0 + k) & 1) == COL) nv[k] = L.rg_a ? (keep ? pc[k] : 0.0) : nv[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k)
+          if (((Q0 + k) & 1) != COL) nv[k] = L.rg_b ? (keep ? pc[k] : 0.0) : nv[k];
+      }
     }
   }
   if constexpr (MASK) {  // the skew's windows (the left / bottom ghosts two half-sweeps late)
@@ -459,6 +475,9 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
     L.rg_a = gx == nx + 1;
     L.rg_b = gx + 1 == nx + 1;
     L.ush_a = gx == 0 ? 2 : 0;
+    L.has_lg = c0 <= 0;
+    L.has_rg = c0 + 127 >= nx + 1;
+    L.rg_in_a = ((nx + 1) & 1) == 0;
   }
   // channel: a tile whose region holds a ghost column (tile-uniform)
   const bool edge = OPEN && (c0 <= 0 || c0 + 127 >= nx + 1);
