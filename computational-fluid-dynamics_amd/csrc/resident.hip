@@ -598,7 +598,7 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
   // this lane's shard has k's bit (every tested k needs one in some shard)
   auto lex_load = [&](int k0, int klast) -> bool {
     const int k = k0 + (lane >> 3), sh = lane & 7;
-    if (k > klast || k % R.check_every != 0) return true;
+    if (k > klast) return true;  // (every iteration, as lexw.hpp / smlex.hip: check_every is the red-black orders')
     const int b = k + R.koff;
     return (ld_bits(R.bits + (size_t)sh * R.bwords + (b >> 6)) >> (b & 63)) & 1ull;
   };

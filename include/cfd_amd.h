@@ -66,7 +66,8 @@ typedef struct cfd_params {
   int print_interval, save_interval;
   double h_inlet, step_x;  /* backwards step geometry */
   int step_i, inlet_jmax;  /* derived step indices (backwards_step-01.cpp:386, 493) */
-  int check_every;      /* residual test every N SOR iterations (1 = reference) */
+  int check_every;      /* residual test every N SOR iterations (1 = reference; red-black orders:
+                           the reference order tests every iteration) */
   int chunk;            /* SOR launches enqueued between host polls (0 = auto) */
   int ordering;         /* CFD_ORDER_LEX (cfd_params_init's default on one device: the reference's own
                            sweep order, bit-identical to the reference binaries - every case at any size,

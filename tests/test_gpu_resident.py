@@ -441,3 +441,28 @@ def test_resident_channel_rb_4096x512_equals_march():
     for n in FIELDS:
         assert_bits(f1[n], f2[n], f"channel rb 4096x512 {n}")
     assert t1.poisson_launches == 1 and t1.proof_fallbacks == 0
+
+
+@pytest.mark.parametrize("order", ["rb", "lex"])
+@pytest.mark.parametrize("case", ["cavity", "channel"])
+def test_resident_check_every_equals_per_launch_paths(case, order):
+    """check_every = 3 through converging solves: red-black tests multiples
+    of 3 only (the resident launch's proofs of the tested iterations, its
+    fallback), the reference order every iteration as lexw.hpp and smlex.hip
+    do - the same counts, residuals and fields as the per-launch kernels."""
+    cp = C.make_params(case, nx=240, ny=80, max_iters=20000)
+    cp.tol_factor = 1e-3
+    out = []
+    for r in (1, 0):
+        g = C.solver_for(cp, ordering=order, small_solve="off", check_every=3, tuning={"resident": r})
+        if case == "cavity":
+            g.applyBoundaryConditions()
+        hist = [g.step() for _ in range(3)]
+        out.append((hist, g.field("p").copy(), g.timing()))
+        g.close()
+    (h1, p1, t1), (h2, p2, t2) = out
+    assert _lib.SOR_KERNEL[t1.sor_kernel] == "resident" and _lib.SOR_KERNEL[t2.sor_kernel] != "resident"
+    assert h1 == h2
+    if order == "rb":
+        assert all(k % 3 == 0 or k == cp.max_iters for k, _ in h1)
+    assert_bits(p1, p2, f"{case} {order} check_every 3 p")
