@@ -211,7 +211,7 @@ def test_reference_order_is_the_default():
     ("cavity/rb", "march_min_th", 24), ("channel/rb", "march_min_th", 16), ("backwards_step/rb", "march_min_th", 24),
     ("cavity", "pair_edge_pct", 80), ("channel", "pair_edge_pct", 45), ("backwards_step", "pair_edge_pct", 45),
     ("cavity", "tile_rounds", 1), ("channel", "tile_rounds", 0), ("rayleigh_benard", "tile_rounds", 1),
-    ("cavity", "tent_th", 64), ("channel", "lexw_edge_pct", 75), ("backwards_step", "lexw_ramp_pct", 0),
+    ("cavity", "tent_th", 64), ("channel", "lexw_edge_pct", 75), ("backwards_step", "lexw_ramp_pct", 100), ("cavity", "lexw_ramp_pct", 0),
     ("cavity@4096", "lexw_edge_pct", 100), ("cavity@1024", "lexw_edge_pct", 75),
     ("backwards_step", "lexw_left", 1), ("cavity", "lexw_left", 1), ("cavity/rb", "resident", 1), ("channel/rb", "resident", 1),
     ("channel", "resident", 1), ("backwards_step", "resident", 0),
