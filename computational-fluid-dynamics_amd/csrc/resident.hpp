@@ -1,25 +1,27 @@
-// resident.hpp — the red-black SOR solve as ONE persistent launch whose
-// workgroups keep their tile of p (and the source) in registers for the whole
-// solve: grids of up to a few million cells (BASELINE configs[1] 1024^2,
-// configs[2] 4096x512).
+// resident.hpp — the SOR solve as ONE persistent launch whose workgroups keep
+// their tile of p (and the source) on chip for the whole solve: grids of up to
+// a few million cells (BASELINE configs[1] cavity 1024^2, configs[2] channel
+// 4096x512), in red-black order and in the reference's own lexicographic
+// order (resident.hip LEX: the skewed half-sweep schedule of lexw.hpp).
 //
 // Why: at these sizes the per-launch designs are bound by fill, not by HBM.
 // The wave march gives each band 8-16 rows against a 15-19-row pipeline; the
 // LDS tiles (tile.hip) reload and store their tile every 4 sweeps and run
 // their sweeps latency- and barrier-bound out of LDS. Here the
-// whole grid lives in the register files of the 256 CUs (1024^2: 8 KB of p
-// and f per wave, ~30 of 128 VGPRs): nothing moves through HBM between
-// sweeps except the tiles' edge bands.
+// whole grid lives in the register files of the 256 CUs: nothing moves
+// through HBM between sweeps except the tiles' edge bands.
 //
-// Layout: one workgroup per tile (at most one per CU, all co-resident: a grid
-// of <= CUs workgroups of up to 16 waves and 65 KB of LDS). A tile owns
-// RES_TW = 112 columns x th rows (ghost rows / columns included at the grid's
-// edges) and holds a region of 128 columns x (th + 2 RES_HALO) rows: lane l of
-// every wave holds the column pair (c0 + 2l, c0 + 2l + 1), wave w the region
-// rows w*RPW .. w*RPW + RPW - 1, in registers (p and f*h^2). A half-sweep
-// updates one colour in place (its neighbours are the other colour): row
-// neighbours within a lane's rows, column neighbours by DPP, the rows of the
-// neighbouring waves through LDS (one barrier per half-sweep).
+// Layout: one workgroup of up to 8 waves per tile (at most one per CU, all
+// co-resident). A tile owns RES_TW = 112 columns x th rows (ghost rows /
+// columns included at the grid's edges) and holds a region of 128 columns x
+// (th + 2 RES_HALO) rows: lane l of every wave holds the column pair
+// (c0 + 2l, c0 + 2l + 1), wave w the region rows w*RPW .. w*RPW + RPW - 1 of p
+// in registers; the source as f*h^2 in registers (cavity, 8-row waves) or as
+// f in LDS (channel: 14-row waves fit 4096x512's 102-row regions). A
+// half-sweep updates one colour in place (its neighbours are the other
+// colour): row neighbours within a lane's rows, column neighbours by DPP, the
+// rows of the neighbouring waves through LDS (one barrier per half-sweep). The
+// channel's ghost refreshes are cells of their own colour with copy rules.
 //
 // Groups: every RES_NS sweeps the tiles exchange their RES_HALO-deep edge
 // bands through global memory (write-through stores, one flag per tile and
@@ -27,21 +29,20 @@
 // halo goes stale by one cell per half-sweep and never reaches the owned
 // cells (RES_HALO = 2 RES_NS), exactly as the fused march launches' halos.
 //
-// Stop rule: proof mode: every tile proves "the reference goes
-// on" for each iteration from its black cells' updates (max |p' - p| against
-// the proof threshold) and marks the iteration proven; a per-group arrival
-// counter says when every tile has contributed. Group g is checked at the
-// start of group g + RES_LAG (no grid barrier on the sweep path). A capped
-// solve (the BASELINE sizes) runs to the cap in this one launch; an iteration
-// no tile proves (near convergence, or non-finite values) ends the launch
-// with code 2 at the group's first iteration k0: the host replays the solve
-// to k0 from its intact input (same launch, checks off) and goes on with the
-// exact-residual launches from there (Solver::solve_resident).
+// Stop rule, with no grid barrier (completion spreads one tile per group, so
+// at group m every tile has finished group m - DIAM):
+//  * red-black: proof mode - tiles prove "the reference goes
+//    on" per iteration from black cells' max |p' - p|; an iteration no tile
+//    proves ends the launch with code 2 at its group's first iteration k0:
+//    the host replays to k0 from the intact input and goes on with the exact
+//    launches (Solver::solve_resident);
+//  * reference order: one sampled row per wave evaluates exact residuals (the
+//    reference's operands) into per-iteration exceedance bits; an iteration
+//    without one hands the solve to lexw.hpp (Solver::solve_resident_lex).
 //
-// Bits: every update is sor_update<CAVITY>'s operations on the same operands
-// in the same order as tile.hip / the march kernels and the oracle's
-// red-black restatement (f*h^2 is precomputed: the same rounding), so p is
-// bit-identical to them.
+// Bits: every update is sor_update's operations on the same operands in the
+// same order as the per-launch kernels and the oracle's restatements (the
+// cavity's f*h^2 precomputed: the same rounding), so p is bit-identical.
 #pragma once
 
 #include "device.hpp"
