@@ -46,6 +46,9 @@
 namespace cfd {
 
 constexpr int LEXW_SHARDS = 8;
+#ifndef CFD_LEXW_RAMP_EDGE_FULL
+#define CFD_LEXW_RAMP_EDGE_FULL 1  // ramp launches: wholly active edge tiles on the unmasked edge march
+#endif
 #ifndef CFD_LEXW_W2
 #define CFD_LEXW_W2 2  // waves per SIMD the steady kernel must fit at NS = 2 (tuned on MI355X)
 #endif
@@ -977,7 +980,10 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
       // tiles of a ramp launch whose every cell is active in every half-sweep
       // it evaluates (H0-1 .. H0+2NS-1) take the unmasked march
       const bool full = smax <= H0 - 2 && Hend <= smin + last;
-      if (edge) { LX_PATH(0); lx_march<CASE, NS, LX_ACT | SM, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      // (wall tiles too: a wholly active one takes the steady launches' edge
+      // march, not the masked one - the masked wall marches set the ramps' time)
+      if (edge && full && CFD_LEXW_RAMP_EDGE_FULL) { LX_PATH(0); lx_march<CASE, NS, SM, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (edge) { LX_PATH(0); lx_march<CASE, NS, LX_ACT | SM, true>(x, lc, L, y0, y1, c0, lane, shard); }
       else if (full) { LX_PATH(1); lx_march<CASE, NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard); }
       else { LX_PATH(2); lx_march<CASE, NS, LX_ACT | SM, false>(x, lc, L, y0, y1, c0, lane, shard); }
     } else {
@@ -1001,7 +1007,14 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     const bool edge = edge_;
     if constexpr (RAMP) {
       const bool full = !rc && smax <= H0 - 2 && Hend <= smin + 2 * (K - 1);
-      if (edge) { LX_PATH(0); lx_march<CASE, NS, LX_ACT | SM, true, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      // an edge march (ghosts, the step's solids) wholly active in every
+      // half-sweep it evaluates, the left / bottom ghosts and the step-column
+      // solids two half-sweeps late included: the steady launches' edge march
+      const bool efull = smax + 2 <= H0 - 2 && Hend <= smin + 2 * (K - 1);
+      if (edge && efull && CFD_LEXW_RAMP_EDGE_FULL) {
+        LX_PATH(0);
+        lx_march<CASE, NS, SM, true, true>(x, lc, L, y0, y1, c0, lane, shard);
+      } else if (edge) { LX_PATH(0); lx_march<CASE, NS, LX_ACT | SM, true, true>(x, lc, L, y0, y1, c0, lane, shard); }
       else if (full) { LX_PATH(1); lx_march<CASE, NS, SM, false, false>(x, lc, L, y0, y1, c0, lane, shard); }
       else if (rc) { LX_PATH(6); lx_march<CASE, NS, LX_ACT | SM, false, true>(x, lc, L, y0, y1, c0, lane, shard); }
       else { LX_PATH(2); lx_march<CASE, NS, LX_ACT | SM, false, false>(x, lc, L, y0, y1, c0, lane, shard); }
