@@ -1016,7 +1016,10 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
         lx_march<CASE, NS, SM, true, true>(x, lc, L, y0, y1, c0, lane, shard);
       } else if (edge) { LX_PATH(0); lx_march<CASE, NS, LX_ACT | SM, true, true>(x, lc, L, y0, y1, c0, lane, shard); }
       else if (full) { LX_PATH(1); lx_march<CASE, NS, SM, false, false>(x, lc, L, y0, y1, c0, lane, shard); }
-      else if (rc) { LX_PATH(6); lx_march<CASE, NS, LX_ACT | SM, false, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (rc && efull && CFD_LEXW_RAMP_EDGE_FULL) {  // (row-checked bands likewise: the steady rc march)
+        LX_PATH(6);
+        lx_march<CASE, NS, SM, false, true>(x, lc, L, y0, y1, c0, lane, shard);
+      } else if (rc) { LX_PATH(6); lx_march<CASE, NS, LX_ACT | SM, false, true>(x, lc, L, y0, y1, c0, lane, shard); }
       else { LX_PATH(2); lx_march<CASE, NS, LX_ACT | SM, false, false>(x, lc, L, y0, y1, c0, lane, shard); }
     } else {
       if (edge) { LX_PATH(0); lx_march<CASE, NS, SM, true, true>(x, lc, L, y0, y1, c0, lane, shard); }
