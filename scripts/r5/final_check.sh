@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
-D=gpurun_out/r5final2; mkdir -p $D
+D=gpurun_out/r5final3; mkdir -p $D
 timeout -k 10 1000 python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu tests > $D/pytest_gpu.log 2>&1
 rc=$?; echo "pytest exit $rc"; tail -n 3 $D/pytest_gpu.log; [ $rc -ne 0 ] && { grep -E "FAIL|Error" $D/pytest_gpu.log | head; exit $rc; }
 timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $D/smoke.log 2>&1
