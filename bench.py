@@ -10,15 +10,18 @@ All inputs are device-resident when the timed region starts.
   value = interior cells x SOR iterations summed over all ranks / wall time of
           the K timed steps (max over ranks), in MLUPS.
 
-Extra fields: steps_per_sec, roofline (the fused red-black SOR kernel, four
-sweeps per launch for the cavity with the proof-mode convergence test, three
-with exact residuals: HIP events on the solver's stream over the timed region; `achieved` = the 24 B/cell one launch must move / launch time,
-`effective_sweep_*` the same per sweep), cpu_baseline (the oracle's
-lexicographic SOR loop — the reference's loop restated in C — on a bounded
-sample of the same grid, rank 0 only), reference_order (N=1: the same
-workload in the reference's lexicographic sweep order, poisson_lexw_kernel,
-bit-identical to the reference's loop; the red-black order of the headline is
-bit-identical to the red-black oracle, and is what splits over GPUs).
+The headline runs the reference's own sweep order (--ordering lex, the
+default at every N: poisson_lexw_kernel, bit-identical to the reference's loop
+on one GPU and on ranks). Extra fields: steps_per_sec, roofline (the SOR
+kernel's steady launches - every cell active -, four sweeps per launch on one
+GPU, three on ranks: HIP events on the solver's stream; `achieved` = the
+24 B/cell one launch must move / launch time, `effective_sweep_*` the same per
+sweep), cpu_baseline (the oracle's lexicographic SOR loop — the reference's
+loop restated in C — on a bounded sample of the same grid, rank 0 only) and,
+at N=1, the same workload in the other order: red_black (red-black SOR with
+the proof-mode test, bit-identical to the red-black oracle; it is not the
+reference's iterate where the solve hits the cap) or, with --ordering rb,
+reference_order.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--global-ny NY]
 For N > 1 launch with torch.distributed.run (one rank per GPU); halos and the
@@ -44,7 +47,9 @@ sys.path.insert(0, os.path.join(ROOT, "computational-fluid-dynamics_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_VALU_PEAK_TF = 78.6  # MI355X fp64 vector spec: half the 157.3 TF fp32 vector rate (MI355X_MICROARCH.md)
-FLOPS_PER_UPDATE = 8.0  # the cavity's SOR update: 3 adds, h^2 f, f subtraction, 2 products, 1 add
+# the cavity's SOR update: 3 adds, h^2 f, f subtraction, 2 products, 1 add (the other cases' updates -
+# an anisotropic sum and a divide - are not priced: no VALU fraction is reported for them)
+FLOPS_PER_UPDATE = {"cavity": 8.0}
 BYTES_PER_CELL = 24.0  # SOR launch: read p_in + read f + write p_out, fp64
 METRIC = "Poisson MLUPS + steps/sec, cavity 4096² @1/2/4/8 GPU; % HBM roofline"
 WORKLOAD = {"cavity": "lid-driven cavity", "channel": "channel flow", "backwards_step": "backwards-facing step",
@@ -127,12 +132,51 @@ def reference_binary(timeout_s: float = 60.0) -> dict | None:
                       f"in {el:.2f} s single-threaded"}
 
 
+def red_black(C, cp, args, device: int, check_every: int, cells_per_launch: int, tuning: dict) -> dict:
+    """The same workload in red-black order (ordering="rb": proof-mode march
+    launches, bit-identical to the red-black oracle; where the solve hits the
+    cap its iterate is not the reference's), timed the same way on one GPU:
+    value, ms per step and the SOR launch's roofline."""
+    import torch
+
+    s = C.solver_for(cp, device=device, check_every=check_every, ordering="rb",
+                     sweeps_per_launch=args.sweeps_per_launch, proof_test=args.proof_test, tuning=tuning)
+    if args.case == "cavity":
+        s.applyBoundaryConditions()
+    s.step()  # warmup
+    s.synchronize()
+    s.reset_timing()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    iters = [s.step()[0] for _ in range(args.lex_steps)]
+    s.synchronize()
+    el = time.perf_counter() - t0
+    tm = s.timing()
+    s.close()
+    sk = _lib_sor_kernel(tm)
+    ns = round(tm.poisson_sweeps / max(tm.poisson_launches, 1))
+    launch_ms = tm.poisson_ms / max(tm.poisson_launches, 1)
+    proof = args.proof_test != "off" and (sk == "tile" or (sk == "march" and ns >= 3))
+    rows = cells_per_launch // (cp.nx + 2)
+    traffic, src = pmc_traffic(args.case, "rb", cp.nx, rows - 2, rows, ns,
+                               sor_template(kcase_of(args.case), sk, ns, proof))
+    achieved = BYTES_PER_CELL * cells_per_launch / (launch_ms * 1e-3) / 1e9
+    return {"ordering": "rb", "value": round(tm.poisson_cell_updates / el / 1e6, 2), "unit": "MLUPS",
+            "ms_per_step": round(el / args.lex_steps * 1e3, 3), "steps": args.lex_steps,
+            "sor_iterations_per_step": iters, "sor_kernel": sk,
+            "template": sor_template(kcase_of(args.case), sk, ns, proof),
+            "sweeps_per_launch": round(tm.poisson_sweeps / max(tm.poisson_launches, 1), 3),
+            "launches_per_step": round(tm.poisson_launches / args.lex_steps, 1),
+            "avg_launch_us": round(launch_ms * 1e3, 2), "achieved_GBs": round(achieved, 1),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src}
+
+
 def reference_order(C, cp, args, device: int, check_every: int, cells_per_launch: int) -> dict:
-    """The same workload in the reference's lexicographic sweep order
-    (ordering="lex": poisson_lexw_kernel, bit-identical to the reference's
-    loop at any size), timed the same way on one GPU: value, ms per step and
-    the steady launches' roofline (every cell active; the ramps at both ends of
-    a solve touch part of the grid)."""
+    """(--ordering rb) The same workload in the reference's lexicographic sweep
+    order (ordering="lex": poisson_lexw_kernel, bit-identical to the
+    reference's loop at any size), timed the same way on one GPU: value, ms per
+    step and the steady launches' roofline (every cell active; the ramps at
+    both ends of a solve touch part of the grid)."""
     import torch
 
     s = C.solver_for(cp, device=device, check_every=check_every, ordering="lex", sweeps_per_launch=args.lex_sweeps)
@@ -198,8 +242,10 @@ def pmc_traffic(case: str, order: str, nx: int, ny: int, rows: int, sweeps: int,
     workload (profiles/r<N>_pmc_<case>_<order>_<nx>x<ny>.json, made by
     scripts/profile_case.sh + pmc_traffic.py), returned only when that file's
     kernel_match is the kernel instance that ran here (same grid rows and
-    sweeps per launch); otherwise None. Second value: the provenance (file,
-    kernel, commit the profile was taken at) or why there is none."""
+    sweeps per launch) and its source hash is that of the kernel's
+    translation unit as built here (cfd_amd.provenance); otherwise None.
+    Second value: the provenance (file, kernel, commit and source hash the
+    profile was taken at) or why there is none."""
     import glob
     import re
 
@@ -222,6 +268,12 @@ def pmc_traffic(case: str, order: str, nx: int, ny: int, rows: int, sweeps: int,
         return None, dict(src, reason=f"kernel mismatch: profile {d.get('kernel_match')!r}, ran {template!r}")
     if not (d.get("nx") == nx and d.get("rows") == rows and d.get("sweeps_per_launch", 1) == sweeps):
         return None, dict(src, reason="grid / sweeps per launch mismatch")
+    # code-exact: the profile's kernel sources must be the ones built here
+    from cfd_amd.provenance import source_hash
+    now = source_hash(template)
+    src["source_hash"] = d.get("source_hash")
+    if d.get("source_hash") is None or d.get("source_hash") != now:
+        return None, dict(src, reason=f"stale: the kernel's sources changed since the profile (now {now})")
     return d.get("hbm_bytes_per_launch"), src
 
 
@@ -257,14 +309,14 @@ def parse_args(argv=None):
     ap.add_argument("--proof-test", default="auto", choices=["auto", "off"],
                     help="red-black launches (every case): proof-mode convergence test (off: exact residual every "
                          "sweep)")
-    ap.add_argument("--ordering", default="rb", choices=["rb", "lex"],
-                    help="SOR sweep order of the headline: rb (red-black: splits over GPUs) or lex (the reference's "
-                         "lexicographic order, bit-identical; one GPU)")
+    ap.add_argument("--ordering", default="lex", choices=["rb", "lex"],
+                    help="SOR sweep order of the headline: lex (default: the reference's lexicographic order, "
+                         "bit-identical to the reference's loop on one GPU and on ranks) or rb (red-black)")
     ap.add_argument("--lex-sweeps", type=int, default=0,
                     help="reference_order: sweeps per lexicographic-order launch (0: auto = 4; 5 for the cavity)")
     ap.add_argument("--lex-steps", type=int, default=2,
-                    help="N=1: also time this many steps in the reference's own (lexicographic) order "
-                         "(0: skip); reported as reference_order")
+                    help="N=1: also time this many steps in the other sweep order (0: skip); reported as "
+                         "red_black (headline lex) or reference_order (headline rb)")
     ap.add_argument("--tile-rounds", type=int, default=-1,
                     help="red-black, one GPU: LDS-tile SOR launches when the grid fits this many resident rounds of "
                          "tiles (0: never; -1: the library default, 1)")
@@ -365,8 +417,6 @@ def run(args, rank: int, world: int, local_rank: int, comm, group, loopback: boo
         from cfd_amd.dist import strip_rows, weak_rows
         comm_info = _comm_info(comm)
         rows = strip_rows(rank, world, ny_global) if strong else weak_rows(rank, args.ny)
-        if args.ordering != "rb":
-            raise SystemExit("the reference's order runs on one GPU (DESIGN.md §5): use --ordering rb with N > 1")
         solver = C.solver_for(cp, device=local_rank, check_every=check_every, rank_rows=rows, comm=comm,
                               sweeps_per_launch=args.sweeps_per_launch, ordering=args.ordering,
                               proof_test=args.proof_test, tuning=tuning)
@@ -494,10 +544,11 @@ def run(args, rank: int, world: int, local_rank: int, comm, group, loopback: boo
             # the register-resident whole-solve launch (resident.hpp): p and f*h^2
             # stay in VGPRs, HBM carries only the tiles' 8-cell edge bands - the
             # bound is the fp64 VALU work and the group hand-offs, not HBM
-            tflops = FLOPS_PER_UPDATE * updates / elapsed / 1e12
+            fpu = FLOPS_PER_UPDATE.get(kcase)
+            tflops = fpu * updates / elapsed / 1e12 if fpu else None
             line["roofline"] = {
-                "bound": "valu", "achieved": round(tflops, 3), "peak": FP64_VALU_PEAK_TF, "unit": "TFLOP/s",
-                "frac": round(tflops / FP64_VALU_PEAK_TF, 4), "traffic": None,
+                "bound": "valu", "achieved": round(tflops, 3) if tflops else None, "peak": FP64_VALU_PEAK_TF,
+                "unit": "TFLOP/s", "frac": round(tflops / FP64_VALU_PEAK_TF, 4) if tflops else None, "traffic": None,
                 "traffic_source": "none: register-resident solve (no per-sweep HBM stream)",
                 "kernel": f"poisson_resident_kernel<{kcase},{'lex' if args.ordering == 'lex' else 'rb'}> "
                           "(whole solve in one launch)",
@@ -511,8 +562,11 @@ def run(args, rank: int, world: int, local_rank: int, comm, group, loopback: boo
             line["cpu_baseline"] = cpu_baseline(cp.nx, cp.ny, args.cpu_seconds, args.case)
             if args.case == "cavity":  # beside it: the reference's own binary on its own case (same host)
                 line["cpu_baseline"]["reference_binary"] = reference_binary()
-        if world == 1 and args.lex_steps > 0 and args.ordering == "rb" and args.case != "rayleigh_benard":
-            line["reference_order"] = reference_order(C, cp, args, local_rank, check_every, cells_per_launch)
+        if world == 1 and args.lex_steps > 0 and args.case != "rayleigh_benard":
+            if args.ordering == "rb":
+                line["reference_order"] = reference_order(C, cp, args, local_rank, check_every, cells_per_launch)
+            else:
+                line["red_black"] = red_black(C, cp, args, local_rank, check_every, cells_per_launch, tuning)
     solver.close()
     return line
 

@@ -66,7 +66,8 @@ class Timing(ctypes.Structure):
                 ("steps", ctypes.c_longlong), ("poisson_sweeps", ctypes.c_longlong),
                 ("poisson_overlapped", ctypes.c_longlong), ("poisson_steady_ms", ctypes.c_double),
                 ("poisson_steady_launches", ctypes.c_longlong),
-                ("proof_fallbacks", ctypes.c_longlong), ("sor_kernel", ctypes.c_int)]
+                ("proof_fallbacks", ctypes.c_longlong), ("sor_kernel", ctypes.c_int),
+                ("resident_timeouts", ctypes.c_longlong)]
 
 
 # every symbol include/cfd_amd.h declares: name -> (restype, argtypes)

@@ -43,9 +43,8 @@ class _SolverBase:
                  ordering: str = "auto", sweeps_per_launch: int = 0, proof_test: str = "auto",
                  small_solve: str = "auto", overlap: str = "auto", tuning: dict[str, int] | None = None):
         """ordering: "lex" (the reference's lexicographic sweep, bit-identical to the
-        reference binaries: the default on one device, strips allowed), "rb" (red-black
-        SOR: the rank path, required with rank_rows) or "auto" (lex on one device, rb
-        on ranks; Rayleigh-Benard, which has no reference solver: rb).
+        reference binaries on one device, on strips and on ranks), "rb" (red-black SOR)
+        or "auto" (lex; Rayleigh-Benard, which has no reference solver: rb).
         sweeps_per_launch: SOR iterations fused per kernel launch (0 = auto: red-black
         4 in proof-mode launches (the step on strips or ranks: 3), 3 (cavity) / 2 (open
         cases) in exact ones; lexicographic 4, 3 on strips); bit-identical either way.
@@ -55,7 +54,7 @@ class _SolverBase:
         if self.params.case_id != self.CASE:
             raise ValueError(f"{type(self).__name__} needs case {CASE_NAMES[self.CASE]}")
         if ordering == "auto":
-            ordering = "rb" if (rank_rows is not None or self.CASE == RAYLEIGH_BENARD) else "lex"
+            ordering = "rb" if self.CASE == RAYLEIGH_BENARD else "lex"
         self.ordering = ordering
         self._cp = to_cparams(self.params, check_every, chunk, ordering, sweeps_per_launch, proof_test,
                               small_solve, overlap)

@@ -134,6 +134,21 @@ __device__ __forceinline__ bool lexw_slot_exceeds(const LexCtl& L, int k) {
   return (w >> (q & 63)) & 1ull;
 }
 
+// Ranks (Solver::lexw_reduce_bits): the exceedance bits of iterations ka .. kb
+// as 0 / 1 doubles, all-reduced with max (= OR over the ranks: the stop rule
+// is "some cell of the whole grid exceeds tol"), then OR-ed back into shard 0,
+// so every rank's launches test the same global bits in the same order.
+__global__ void lexw_bits_gather_kernel(LexCtl L, int ka, int kb, double* __restrict__ flags) {
+  const int k = ka + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (k <= kb) flags[k - ka] = lexw_slot_exceeds(L, k) ? 1.0 : 0.0;
+}
+__global__ void lexw_bits_scatter_kernel(LexCtl L, int ka, int kb, const double* __restrict__ flags) {
+  const int k = ka + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (k > kb || !(flags[k - ka] > 0.0)) return;
+  const int q = L.kmax + k;
+  atomicOr(L.bits + (q >> 6), 1ull << (q & 63));
+}
+
 // the reference's while condition for the slots [ka, kb] completed since the
 // last test (0 = the primed initial residual): false = stop (recorded once).
 // A slot below kexact holds the sampled rows only: no exceedance there proves

@@ -2,8 +2,13 @@
 // design): red-black with the proof-mode stop rule, and the reference's own
 // order with sampled exceedance bits. Own translation unit: device.hpp only.
 #include <algorithm>
+#include <mutex>
+#include <set>
+#include <string>
 #include <type_traits>
+#include <utility>
 
+#include "internal.hpp"
 #include "resident.hpp"
 
 namespace cfd {
@@ -970,32 +975,66 @@ ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open) {
   return rp;
 }
 
+namespace {
+using ResKernel = void (*)(Geo, Coef, const double*, double*, const double*, ResCtl, ResPlan, int);
+
+// the kernel instance of a (case, order, rows per wave) and its dynamic LDS
+// (the channel's source), or nullptr: no instance for that pair
+ResKernel res_kernel(int case_id, bool lex, int rpw, size_t* lds) {
+  *lds = 0;
+  if (case_id == CAVITY && rpw == 8)
+    return lex ? poisson_resident_kernel<CAVITY, 8, true> : poisson_resident_kernel<CAVITY, 8, false>;
+  if (case_id == CHANNEL && rpw == 8) {
+    *lds = res_flds_bytes<8>();
+    return lex ? poisson_resident_kernel<CHANNEL, 8, true> : poisson_resident_kernel<CHANNEL, 8, false>;
+  }
+  if (case_id == CHANNEL && rpw == RES_RPW_OPEN) {
+    *lds = res_flds_bytes<RES_RPW_OPEN>();
+    return lex ? poisson_resident_kernel<CHANNEL, RES_RPW_OPEN, true>
+               : poisson_resident_kernel<CHANNEL, RES_RPW_OPEN, false>;
+  }
+  return nullptr;
+}
+
+// dynamic LDS past the static 64 KB needs an attribute per kernel instance and
+// device, set once each (its result checked)
+void res_kernel_attr(ResKernel k, size_t lds) {
+  if (lds == 0) return;
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) throw Error(CFD_E_DEVICE, "resident solve: hipGetDevice failed");
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.count({reinterpret_cast<const void*>(k), dev})) return;
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)lds);
+  if (e != hipSuccess)
+    throw Error(CFD_E_DEVICE, std::string("resident solve: hipFuncSetAttribute: ") + hipGetErrorString(e));
+  done.insert({reinterpret_cast<const void*>(k), dev});
+}
+}  // namespace
+
+int res_coresident_tiles(int case_id, bool lex, const ResPlan& rp, int n_cu) {
+  size_t lds = 0;
+  const ResKernel k = res_kernel(case_id, lex, rp.rpw, &lds);
+  if (!k || rp.waves <= 0) return 0;
+  res_kernel_attr(k, lds);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k), rp.waves * 64, lds) !=
+      hipSuccess)
+    return 0;
+  return per_cu * n_cu;
+}
+
 void res_launch(int case_id, bool lex, const Geo& g, const Coef& c, const double* pin, double* pout, const double* f,
                 const ResCtl& R, const ResPlan& rp, int flags, hipStream_t st) {
   const int n = rp.ctiles * rp.rtiles;
-  if (n <= 0) return;
-  const dim3 grid(n), block(rp.waves * 64);
-  if (case_id == CAVITY && rp.rpw == 8) {
-    if (lex) poisson_resident_kernel<CAVITY, 8, true><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
-    else poisson_resident_kernel<CAVITY, 8, false><<<grid, block, 0, st>>>(g, c, pin, pout, f, R, rp, flags);
-  } else if (case_id == CHANNEL) {
-    // (the source in dynamic LDS: past the static 64 KB, an attribute per kernel)
-    auto go = [&](auto kern, size_t lds) {
-      static bool set = false;
-      if (!set) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        set = true;
-      }
-      kern<<<grid, block, lds, st>>>(g, c, pin, pout, f, R, rp, flags);
-    };
-    if (lex) {
-      if (rp.rpw == 8) go(poisson_resident_kernel<CHANNEL, 8, true>, res_flds_bytes<8>());
-      else if (rp.rpw == RES_RPW_OPEN) go(poisson_resident_kernel<CHANNEL, RES_RPW_OPEN, true>, res_flds_bytes<RES_RPW_OPEN>());
-    } else {
-      if (rp.rpw == 8) go(poisson_resident_kernel<CHANNEL, 8, false>, res_flds_bytes<8>());
-      else if (rp.rpw == RES_RPW_OPEN) go(poisson_resident_kernel<CHANNEL, RES_RPW_OPEN, false>, res_flds_bytes<RES_RPW_OPEN>());
-    }
-  }
+  if (n <= 0) throw Error(CFD_E_STATE, "resident solve: empty plan");
+  size_t lds = 0;
+  const ResKernel k = res_kernel(case_id, lex, rp.rpw, &lds);
+  if (!k) throw Error(CFD_E_STATE, "resident solve: no kernel instance for this case / rows per wave");
+  res_kernel_attr(k, lds);
+  k<<<dim3(n), dim3(rp.waves * 64), lds, st>>>(g, c, pin, pout, f, R, rp, flags);
 }
 
 }  // namespace cfd

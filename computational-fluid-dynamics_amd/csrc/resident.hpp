@@ -94,6 +94,11 @@ inline size_t res_state_words(int tiles, int K) {
   const size_t n = (size_t)tiles + (size_t)K + 1 + 8;
   return (n + 3) / 4 * 4;
 }
+// tiles of plan rp that can be resident at once on n_cu CUs (occupancy of the
+// kernel instance with its LDS; 0: no instance): the persistent launch's
+// workgroups spin on each other, so a plan above this must not launch
+int res_coresident_tiles(int case_id, bool lex, const ResPlan& rp, int n_cu);
+// throws cfd::Error when the pair has no kernel instance
 void res_launch(int case_id, bool lex, const Geo& g, const Coef& c, const double* pin, double* pout, const double* f,
                 const ResCtl& R, const ResPlan& rp, int flags, hipStream_t st);
 // LEX exceedance-bit words per shard for K iterations on an nx x ny grid, and the bit offset

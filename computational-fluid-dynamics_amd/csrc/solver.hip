@@ -166,8 +166,10 @@ class Solver {
     tplan = tile_plan(P.nx, g.wj0, g.wj1 + 1, tile_rounds * n_cu);
     tile_on = tplan.ctiles > 0;
   }
-  // Register-resident whole-solve launch (resident.hpp): red-black cavity, one
-  // strip, no ranks, proof mode, a grid of at most one tile per CU
+  // Register-resident whole-solve launch (resident.hpp): the cavity and the
+  // channel, one strip, no ranks, both orders (red-black with proof mode), a
+  // grid of at most one tile per CU whose tiles can all be resident at once
+  // (the occupancy of the kernel instance: its workgroups wait on each other)
   // (CFD_TUNE_RESIDENT). Its exchange fields and state words are allocated at
   // the first solve.
   bool res_knob = false;
@@ -190,7 +192,9 @@ class Solver {
     if (P.ordering == CFD_ORDER_RB && (!proof_enabled || !(C.proof_k > 0.0))) return;
     const Geo& g = S[0].g;
     rplan = res_plan(P.nx, g.wj0, g.wj1 + 1, n_cu, open);
-    res_on = rplan.ctiles > 0;
+    res_on = rplan.ctiles > 0 &&
+             rplan.ctiles * rplan.rtiles <= res_coresident_tiles(open ? CHANNEL : CAVITY, P.ordering == CFD_ORDER_LEX,
+                                                                 rplan, n_cu);
   }
   struct LaunchRec {
     int first, n;        // iterations first .. first+n-1
@@ -280,11 +284,60 @@ class Solver {
            (P.case_id == CFD_CAVITY || P.case_id == CFD_CHANNEL || (P.case_id == CFD_BACKSTEP && step_lexw_ok()));
   }
   double* cscr = nullptr;  // the step's deferred corner residual across launches (LexCtl::cscr)
-  // sweeps per reference-order launch: 4 (auto) on one strip; strips keep 3
-  // (their 8-row halos serve up to 3, lexw.hpp lexw_twc); the cavity also 1-3
+  // sweeps per reference-order launch: 4 (auto) on one strip; strips and
+  // ranks keep 3 (their 8-row halos serve up to 3, lexw.hpp lexw_twc); the
+  // cavity also 1-3
   int lexw_ns() const {
     const int ns = (P.case_id != CFD_CAVITY || P.sweeps_per_launch < 1) ? 4 : P.sweeps_per_launch;
-    return S.size() > 1 ? std::min(ns, 3) : ns;
+    return multi() ? std::min(ns, 3) : ns;
+  }
+  bool ranks() const { return comm && comm->nranks > 1; }
+  // Reference order on ranks: the exceedance bits of the iterations every
+  // cell has contributed to are OR-ed over the ranks (lexw_bits_gather /
+  // scatter around a max all-reduce) every LEXW_RED_EVERY launches, before the
+  // launches that test them; a stop found up to that many launches late costs
+  // nothing but those launches (a stop is replayed from the initial field).
+  static constexpr int LEXW_RED_EVERY = 8;
+  double* lexflags = nullptr;  // K + 1 doubles: the all-reduced bits
+  size_t lexflags_n = 0;
+  void lexw_reduce_bits(const LexCtl& L, int ka, int kb) {
+    if (!ranks() || ka > kb) return;
+    const int n = kb - ka + 1;
+    if ((size_t)n > lexflags_n) throw Error(CFD_E_STATE, "lexicographic ordering: bit reduction range");
+    lexw_bits_gather_kernel<<<(n + 255) / 256, 256, 0, st>>>(L, ka, kb, lexflags);
+    check_launch("lexw_bits_gather");
+    comm_allreduce_max(comm, lexflags, (size_t)n, st);
+    lexw_bits_scatter_kernel<<<(n + 255) / 256, 256, 0, st>>>(L, ka, kb, lexflags);
+    check_launch("lexw_bits_scatter");
+  }
+  // The reference order's sequential sums on ranks (the open cases' source
+  // sum, channel-01.cpp:620-628 / backwards_step-01.cpp:843-862, and the
+  // kinetic energy of the statistics, cavity-01.cpp:750-755): one chain of
+  // dependent adds in the reference's loop order (rows ascending). Ranks own
+  // consecutive row blocks in rank order, so rank r continues from rank r-1's
+  // running sum (a one-double send / recv per link) and the last rank's
+  // total goes back to every rank: the same bits as one device. Every rank
+  // issues the same group sequence (the loopback transport needs it; RCCL
+  // takes the empty groups as no-ops).
+  void seq_sum_ranks(int a, int b, int mode, double* acc) {
+    const int R = comm->nranks, me = comm->rank;
+    const Strip& s = S[0];
+    for (int q = 0; q < R; ++q) {
+      if (q == me) seq_sum_launch(s.g, C, s.b[a], b >= 0 ? s.b[b] : nullptr, mode, acc, me > 0, st);
+      if (q + 1 < R) {
+        comm_group_start(comm);
+        if (me == q) comm_send(comm, acc, 1, q + 1, st);
+        if (me == q + 1) comm_recv(comm, acc, 1, q, st);
+        comm_group_end(comm, st);
+      }
+    }
+    comm_group_start(comm);
+    if (me == R - 1) {
+      for (int p = 0; p < R - 1; ++p) comm_send(comm, acc, 1, p, st);
+    } else {
+      comm_recv(comm, acc, 1, R - 1, st);
+    }
+    comm_group_end(comm, st);
   }
   // rows one lexw wave marches beyond its band: the pipeline (2NS+1 each side) + parity row
   static int lexw_extra(int ns) { return 2 * (2 * ns + 1) + 1; }
@@ -498,6 +551,9 @@ class Solver {
     ring = srcmax = divmax = tolv = total = partials = resmax = cscr = nullptr;
     if (lexbits) (void)hipFree(lexbits);
     lexbits = nullptr;
+    if (lexflags) (void)hipFree(lexflags);
+    lexflags = nullptr;
+    lexflags_n = 0;
     if (smlex_ck) (void)hipFree(smlex_ck);
     smlex_ck = nullptr;
     for (auto*& x : res_x) {
@@ -554,10 +610,6 @@ class Solver {
     for (int sw : {P.proof_test, P.small_solve, P.overlap})
       if (sw < CFD_AUTO || sw > CFD_OFF) throw Error(CFD_E_ARG, "proof_test / small_solve / overlap must be a cfd_switch");
     if (P.ordering != CFD_ORDER_RB && P.ordering != CFD_ORDER_LEX) throw Error(CFD_E_ARG, "unknown ordering");
-    // (the reference order's dependency chain spans the whole grid: one device,
-    // DESIGN.md §5; a rank solver is rejected here, before it allocates)
-    if (P.ordering == CFD_ORDER_LEX && comm)
-      throw Error(CFD_E_ARG, "lexicographic ordering runs on one device (strips allowed), not on ranks");
     // (the cavity's lexicographic solve runs on the multi-block wavefront kernel
     // at any size; the open cases on the one-workgroup kernel)
     if (P.ordering == CFD_ORDER_LEX && P.case_id == CFD_BACKSTEP && !step_lexw_ok() && (P.nx + P.ny) / 3 + 8 >= LEX_WIN)
@@ -565,9 +617,9 @@ class Solver {
                              "supports nx + ny < 12000");
     // (that step runs the one-workgroup kernel, solve_lex: one strip; rejected
     // here rather than at the first solve)
-    if (P.ordering == CFD_ORDER_LEX && P.case_id == CFD_BACKSTEP && !step_lexw_ok() && nstrips > 1)
+    if (P.ordering == CFD_ORDER_LEX && P.case_id == CFD_BACKSTEP && !step_lexw_ok() && (nstrips > 1 || comm))
       throw Error(CFD_E_ARG, "lexicographic ordering of a backwards step with a block under 2 cells wide or high "
-                             "runs on one strip (n_strips = 1)");
+                             "runs on one strip (n_strips = 1, no ranks)");
 #if CFD_WT_STORE
     // (write-through p_out stores address a strip's buffer with 32-bit buffer records)
     if ((double)(P.ny + 2 * HALO + 2) * (double)(((P.nx + 3) + 15) / 16 * 16) * 8.0 >= 4294967295.0)
@@ -673,14 +725,16 @@ class Solver {
       check_launch("source");
     }
     if (P.case_id != CFD_CAVITY) {
-      if (P.ordering == CFD_ORDER_LEX) {  // the reference's sequential sum, bit for bit (strips in order)
+      if (P.ordering == CFD_ORDER_LEX && ranks()) {  // the same chain, rank to rank
+        seq_sum_ranks(B_F, -1, 0, total);
+      } else if (P.ordering == CFD_ORDER_LEX) {  // the reference's sequential sum, bit for bit (strips in order)
         for (size_t q = 0; q < S.size(); ++q)
           seq_sum_launch(S[q].g, C, S[q].b[B_F], nullptr, 0, total, q > 0, st);
       } else {
         sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total);
       }
       check_launch("sum_partials");
-      if (comm && comm->nranks > 1) comm_allreduce_sum(comm, total, 1, st);
+      if (ranks() && P.ordering != CFD_ORDER_LEX) comm_allreduce_sum(comm, total, 1, st);
       for (auto& s : S) {
         subtract_mean_kernel<<<s.grid2d, 256, 0, st>>>(s.g, C, s.b[B_F], total, fluid_count, srcmax);
         check_launch("subtract_mean");
@@ -1201,13 +1255,28 @@ class Solver {
       plans[q] = multi_plan(S[q].g.wj0, S[q].g.wj1 + 1, 0, 0, resident_lexw_waves / (int)S.size(), ns,
                             ns >= 5 ? 90 : 96,  // (a wave's march steps + 9 <= 127: its iterations fit one 64-bit mask)
                             lexw_edge_pct, lexw_twc(ns), lexw_extra(ns));
-    // steady launches: every cell active in every half-sweep of the launch and
-    // of the previous one's last (nx+ny+1 <= H0 <= 2K-2NS+1, H0 = 2 + 2NS m)
-    const int ms0 = (P.nx + P.ny - 1 + 2 * ns - 1) / (2 * ns), ms1 = floordiv(2 * K - 2 * ns - 1, 2 * ns);
+    // steady launches of strip q: every cell the strip's launch touches (its
+    // rows and the HALO rows on each side: i + j in [smin, smax]) active in
+    // every half-sweep of the launch and of the previous one's last
+    // (smax + 1 <= H0 <= smin + 2K - 2NS - 1, H0 = 2 + 2NS m; one strip:
+    // smin = 2, smax = nx + ny). A strip of a tall grid (ranks) runs its own
+    // steady window instead of the whole grid's, which starts only once the
+    // last row has started.
+    std::vector<int> qs0(S.size()), qs1(S.size());
+    int ms0 = 0, ms1 = INT32_MAX;  // launches steady on every strip (timed)
+    for (size_t q = 0; q < S.size(); ++q) {
+      const Geo& g = S[q].g;
+      const int smax = P.nx + std::min(P.ny, g.j1 + HALO), smin = 1 + std::max(1, g.j0 - HALO);
+      qs0[q] = (smax - 1 + 2 * ns - 1) / (2 * ns);
+      qs1[q] = floordiv(smin + 2 * K - 2 * ns - 3, 2 * ns);
+      ms0 = std::max(ms0, qs0[q]);
+      ms1 = std::min(ms1, qs1[q]);
+    }
     const bool steady = time_steady && ms1 >= ms0;
     const int chunk = P.chunk > 0 ? P.chunk : 32;
     if (K >= 1) lexw_presolid();  // (both buffers hold the solve's input here)
     int tested = tests ? ka0 - 1 : K;  // highest iteration tested
+    int reduced = tested;              // ranks: highest iteration whose bits are OR-ed over the ranks
     bool stopped = false;
     int m = 0, c = 0;
     *kstop = -1;
@@ -1221,6 +1290,13 @@ class Solver {
           } else {
             ka = tested + 1;
             kb = std::min(lexw_done(m - 1, ns), K - 1);
+            if (ranks()) {  // (only bits OR-ed over the ranks are tested)
+              if (m % LEXW_RED_EVERY == 0 && kb > reduced) {
+                lexw_reduce_bits(L, reduced + 1, kb);
+                reduced = kb;
+              }
+              kb = std::min(kb, reduced);
+            }
           }
           if (ka <= kb) tested = kb;
         }
@@ -1228,7 +1304,7 @@ class Solver {
         if (multi()) exchange(bin, HALO);
         if (steady && m == ms0) HIPC(hipEventRecord(ev_f0, st));
         for (size_t q = 0; q < S.size(); ++q)
-          launch_lexw(ns, m >= ms0 && m <= ms1, m < m_full, plans[q], S[q].g, S[q].b[bin], S[q].b[bout],
+          launch_lexw(ns, m >= qs0[q] && m <= qs1[q], m < m_full, plans[q], S[q].g, S[q].b[bin], S[q].b[bout],
                       S[q].b[B_F], L, 2 + 2 * ns * m, K, ka, kb, !tests, resident_lexw_waves / (int)S.size());
         check_launch("poisson_lexw");
         if (steady && m == ms1) HIPC(hipEventRecord(ev_f1, st));
@@ -1250,6 +1326,10 @@ class Solver {
         *kstop = h_stat[1];
         *code = h_stat[0];
       } else if (tested < K - 1) {  // iterations completed by the last launches: tested here, in order
+        if (ranks() && reduced < K - 1) {
+          lexw_reduce_bits(L, std::max(reduced + 1, 1), K - 1);
+          HIPC(hipStreamSynchronize(st));
+        }
         std::vector<unsigned long long> hb(lexbits_words);
         HIPC(hipMemcpy(hb.data(), lexbits, lexbits_words * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         const size_t wps = lexbits_words / LEXW_SHARDS;
@@ -1327,8 +1407,12 @@ class Solver {
     return (base + n) % 2;
   }
 
+  // On ranks (a strip per process) the same launches run on every rank, the
+  // halo rows exchanged before each; the stop rule reads exceedance bits OR-ed
+  // over the ranks (lexw_reduce_bits) and every host decision (stop, replay,
+  // exact fallback) derives from all-reduced values, so all ranks take the
+  // same path and issue the same RCCL sequence.
   void solve_lexw(cfd_step_info* out) {
-    if (comm) throw Error(CFD_E_STATE, "lexicographic ordering on ranks is not implemented (use strips on one device)");
     const int ns = lexw_ns();
     const int K = P.max_iters;
     const int base = pcur & 1;
@@ -1350,6 +1434,12 @@ class Solver {
       lexbits = nullptr;
       HIPC(hipMalloc(&lexbits, words * sizeof(unsigned long long)));
       lexbits_words = words;
+    }
+    if (ranks() && lexflags_n < (size_t)K + 1) {
+      if (lexflags) HIPC(hipFree(lexflags));
+      lexflags = nullptr;
+      HIPC(hipMalloc(&lexflags, ((size_t)K + 1) * sizeof(double)));
+      lexflags_n = (size_t)K + 1;
     }
     lex_reset_tests();
     HIPC(hipEventRecord(ev_a, st));
@@ -1617,6 +1707,7 @@ class Solver {
     R.K = K;
     R.check_every = std::max(1, P.check_every);
     HIPC(hipMemsetAsync(res_state, 0, words * sizeof(unsigned), st));
+    HIPC(hipMemsetAsync(R.status, 0xff, sizeof(int), st));  // (-1 until the launch sets its status)
     HIPC(hipEventRecord(ev_a, st));
     res_launch(cid, false, s.g, C, pin, pout, s.b[B_F], R, rplan, 0, st);
     check_launch("poisson (resident)");
@@ -1629,7 +1720,15 @@ class Solver {
     HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
     T.poisson_ms += ms;
     T.poisson_launches += 1;
-    if (timeout) throw Error(CFD_E_STATE, "resident SOR solve: a tile's wait timed out (tiles not co-resident?)");
+    // a wait that timed out (tiles not co-resident after all): nothing but the
+    // exchange fields and p_out was written, p_in is intact - the exact
+    // launches take the whole solve
+    if (timeout) {
+      ++T.resident_timeouts;
+      k0 = 0;
+      return false;
+    }
+    if (code == -1) throw Error(CFD_E_STATE, "resident SOR solve: the launch set no status");
     if (code == 0 || code == 1) {
       const int iters = code == 0 ? K : 0;
       double res;
@@ -1665,7 +1764,10 @@ class Solver {
       HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
       T.poisson_ms += ms;
       T.poisson_launches += 1;
-      if (h_stat[2]) throw Error(CFD_E_STATE, "resident SOR replay: a tile's wait timed out");
+      if (h_stat[2]) {  // (as above: the exact launches from scratch)
+        ++T.resident_timeouts;
+        k0 = 0;
+      }
     }
     return false;
   }
@@ -1721,6 +1823,7 @@ class Solver {
     R.koff = res_lex_koff(P.nx, P.ny);
     HIPC(hipMemsetAsync(res_state, 0, words * sizeof(unsigned), st));
     HIPC(hipMemsetAsync(res_bits, 0, bn * sizeof(unsigned long long), st));
+    HIPC(hipMemsetAsync(R.status, 0xff, sizeof(int), st));  // (-1 until the launch sets its status)
     HIPC(hipEventRecord(ev_a, st));
     res_launch(P.case_id == CFD_CHANNEL ? CHANNEL : CAVITY, true, s.g, C, pin, pout, s.b[B_F], R, rplan, 0, st);
     check_launch("poisson (resident, reference order)");
@@ -1732,7 +1835,10 @@ class Solver {
     HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
     T.poisson_ms += ms;
     T.poisson_launches += 1;
-    if (timeout) throw Error(CFD_E_STATE, "resident SOR solve: a tile's wait timed out (tiles not co-resident?)");
+    if (timeout) {  // (tiles not co-resident after all: p_in is intact, the exact path takes the solve)
+      ++T.resident_timeouts;
+      return false;
+    }
     if (code == 2) {
       ++T.proof_fallbacks;
       return false;
@@ -2009,14 +2115,16 @@ class Solver {
                                                        partials + s.part_off, divmax);
       check_launch("centers_stats");
     }
-    if (P.ordering == CFD_ORDER_LEX)
+    if (P.ordering == CFD_ORDER_LEX && ranks())
+      seq_sum_ranks(B_UC, B_VC, 1, total + 1);
+    else if (P.ordering == CFD_ORDER_LEX)
       for (size_t q = 0; q < S.size(); ++q)
         seq_sum_launch(S[q].g, C, S[q].b[B_UC], S[q].b[B_VC], 1, total + 1, q > 0, st);
     else
       sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total + 1);
     check_launch("sum_partials");
-    if (comm && comm->nranks > 1) {
-      comm_allreduce_sum(comm, total + 1, 1, st);
+    if (ranks()) {
+      if (P.ordering != CFD_ORDER_LEX) comm_allreduce_sum(comm, total + 1, 1, st);
       comm_allreduce_max(comm, divmax, RES_SHARDS * SHARD_STRIDE, st);
     }
     double ke = 0;
@@ -2171,10 +2279,11 @@ cfd_solver* cfd_create_rank(const cfd_params* p, int device, int row_begin, int 
   cfd_solver* out = nullptr;
   guard([&] {
     if (!p) throw Error(CFD_E_ARG, "null params");
-    // (cfd_params_init selects the reference order, which runs on one device: DESIGN.md §5)
-    if (p->ordering == CFD_ORDER_LEX)
-      throw Error(CFD_E_ARG, "lexicographic ordering runs on one device (strips allowed), not on ranks: "
-                             "cfd_create_rank needs ordering = CFD_ORDER_RB");
+    // (Solver::validate: the one-workgroup reference-order kernel of a thin step block needs one strip)
+    if (p->ordering == CFD_ORDER_LEX && p->case_id == CFD_BACKSTEP &&
+        !(p->step_i >= 2 && p->inlet_jmax >= 1 && p->inlet_jmax <= p->ny - 2))
+      throw Error(CFD_E_ARG, "lexicographic ordering of a backwards step with a block under 2 cells wide or high "
+                             "runs on one strip (n_strips = 1, no ranks)");
     if (row_begin < 1 || row_end > p->ny || row_end - row_begin + 1 < cfd::HALO)
       throw Error(CFD_E_ARG, "rank rows must lie in [1, ny] and span at least 8 rows (the SOR halo depth)");
     // the halo exchange talks to ranks rank-1 (rows below) and rank+1 (rows

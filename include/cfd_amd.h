@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 11
+#define CFD_AMD_ABI_VERSION 12
 
 /* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
  * tree (only figures): it is the cavity's projection step with a resting lid
@@ -69,10 +69,11 @@ typedef struct cfd_params {
   int check_every;      /* residual test every N SOR iterations (1 = reference; red-black orders:
                            the reference order tests every iteration) */
   int chunk;            /* SOR launches enqueued between host polls (0 = auto) */
-  int ordering;         /* CFD_ORDER_LEX (cfd_params_init's default on one device: the reference's own
-                           sweep order, bit-identical to the reference binaries - every case at any size,
-                           strips on one device allowed) or CFD_ORDER_RB (red-black: the rank path, and
-                           faster where the reference's solve converges; required by cfd_create_rank) */
+  int ordering;         /* CFD_ORDER_LEX (cfd_params_init's default: the reference's own sweep order,
+                           bit-identical to the reference binaries - every case at any size, on strips of
+                           one device and on ranks (ABI 12): the same bits at every strip / rank count) or
+                           CFD_ORDER_RB (red-black: faster where the reference's solve converges, and its
+                           rank launches overlap the halo exchange with the interior rows) */
   int sweeps_per_launch; /* SOR iterations fused into one kernel launch, bit-identical for every value:
                            0 = auto: red-black with the proof-mode test 4 (the backwards step on strips or
                            ranks: 3), red-black with exact residuals 3 (cavity) / 2 (channel, step);
@@ -125,6 +126,8 @@ typedef struct cfd_timing {
   long long proof_fallbacks;  /* red-black cavity: solves whose proof-mode convergence test left an
                                  iteration open, finished with exact residuals */
   int sor_kernel;             /* enum cfd_sor_kernel: the SOR kernel family of the last solve (ABI 8) */
+  long long resident_timeouts; /* resident whole-solve launches whose tiles' waits timed out (never expected:
+                                  the plan checks co-residency); the exact launches took those solves (ABI 12) */
 } cfd_timing;
 
 /* Which SOR kernel family ran a solve (cfd_timing.sor_kernel); every one gives the same bits for
@@ -139,8 +142,9 @@ enum cfd_sor_kernel {
                          the other reference-order kernels do not take) */
   CFD_SOR_SMLEX = 6,  /* reference order, whole solve in one workgroup, p in LDS (smlex.hip): reference-sized
                          grids (ABI 9) */
-  CFD_SOR_RESIDENT = 7 /* red-black whole solve in one persistent launch, every tile of p in registers
-                          (resident.hpp): one strip of up to ~2 M cells (ABI 11) */
+  CFD_SOR_RESIDENT = 7 /* whole solve in one persistent launch, every tile of p in registers (resident.hpp):
+                          the cavity and the channel, both orders, one strip of up to ~2 M cells, no ranks
+                          (ABI 11) */
 };
 
 /* Library / ABI info. */
@@ -166,7 +170,10 @@ cfd_solver* cfd_create(const cfd_params* p, int device, int n_strips);
 
 /* Multi-process construction: this rank owns interior rows
  * [row_begin, row_end] (1-based, inclusive) of the global grid; neighbour
- * halos travel over RCCL (see cfd_comm_*). */
+ * halos travel over RCCL (see cfd_comm_*). Both orderings (ABI 12: the
+ * reference's order too - halo rows before every launch, the stop rule's
+ * exceedance bits OR-ed over the ranks, the sequential sums chained rank to
+ * rank: bit-identical to one device). */
 cfd_solver* cfd_create_rank(const cfd_params* p, int device, int row_begin, int row_end, void* comm);
 int cfd_destroy(cfd_solver* s);
 
@@ -229,9 +236,12 @@ enum cfd_tuning {
   CFD_TUNE_LEXW_LEFT = 10,    /* reference-order backwards step: 1 = the column tiles left of the step's column end
                                  at the block's bottom row and march as a channel below it (default), 0 = the
                                  per-cell masked march over every row that reaches the block (ABI 10) */
-  CFD_TUNE_RESIDENT = 11      /* red-black cavity, one strip, proof mode: 1 = the whole solve as one persistent
-                                 register-resident launch where the grid fits one tile per CU (default for the
-                                 cavity: 1024^2 2.2 us per sweep against the LDS tiles' 5.2), 0 = never (ABI 11) */
+  CFD_TUNE_RESIDENT = 11      /* the cavity and the channel, one strip, no ranks, both orders (red-black: with the
+                                 proof-mode test; the reference order: sampled exceedance bits, an iteration they
+                                 leave open finished by the multi-block march): 1 = the whole solve as one
+                                 persistent register-resident launch where the grid fits one tile per CU and every
+                                 tile can be resident at once (default: cavity 1024^2 2.2 us per sweep against the
+                                 LDS tiles' 5.2), 0 = never (ABI 11) */
 };
 int cfd_set_tuning(cfd_solver* s, int knob, int value);
 /* The default a solver created from these parameters starts with (host only, no

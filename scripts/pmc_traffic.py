@@ -4,13 +4,17 @@ per launch with the gfx950 corrections (FETCH_SIZE x2 for 16-B/lane streaming
 reads, WRITE_SIZE exact for 16-B/lane stores: MI355X_MICROARCH.md, HBM
 [CDNA4]). CFD_COMMIT (the git commit of the profiled tree, set by the caller:
 the GPU box has no .git) is recorded as "commit"; bench.py reports it as the
-traffic's provenance. usage: pmc_traffic.py DIR KERNEL_SUBSTRING OUT.json [NX] [SWEEPS_PER_LAUNCH] [NY]"""
+traffic's provenance, with the kernel's source hash. usage: pmc_traffic.py DIR KERNEL_SUBSTRING OUT.json [NX] [SWEEPS_PER_LAUNCH] [NY]"""
 import csv
 import glob
 import json
 import os
 import statistics
 import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "computational-fluid-dynamics_amd"))
+from cfd_amd.provenance import source_hash  # noqa: E402
 
 d, ksub, out = sys.argv[1], sys.argv[2], sys.argv[3]
 nx = int(sys.argv[4]) if len(sys.argv) > 4 else 4096
@@ -44,6 +48,9 @@ res = {"kernel_match": ksub, "nx": nx, "ny": ny, "rows": rows, "sweeps_per_launc
        "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wb, "hbm_bytes_per_launch": rd + wb,
        "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": (rd + wb) / alg,
        "commit": os.environ.get("CFD_COMMIT") or None,
+       # sha256 of the kernel's translation-unit sources on the profiled tree
+       # (cfd_amd.provenance): bench.py drops the traffic when the sources changed
+       "source_hash": source_hash(ksub),
        "command": f"scripts/pmc_traffic.sh (rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE, separate passes), {d}"}
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

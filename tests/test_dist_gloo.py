@@ -301,3 +301,161 @@ def test_two_rank_proof_launches_equal_single_domain(tol, cap):
     if 0.0 < tol < 1e9:
         assert len(fb[0]) >= 1  # converging: the last iterations are evaluated exactly
         assert out[0][6] > 0  # the lower rank alone would have fallen back earlier
+
+
+# ---- the reference's order on ranks (Solver::solve_lexw with a communicator) ----
+#
+# The lexicographic sweep (cavity-01.cpp:640-656) as the skewed half-sweep
+# schedule the GPU runs (csrc/lexw.hpp: cell (j, i) performs its iteration k
+# at half-sweep i + j + 2(k - 1)), on two gloo ranks: HALO rows exchanged
+# before every launch of 3 sweeps (6 half-sweeps, the halo rows recomputed
+# redundantly), each cell's iteration-k residual evaluated in the half-sweep
+# after its update (W, S before it, E, N after: the reference's operands), one
+# exceedance bit per iteration per rank, OR-ed over the ranks with a max
+# all-reduce (Solver::lexw_reduce_bits), the stop at the first iteration
+# without one and the replay of that many iterations from the initial field.
+# Must equal the reference's loop on one domain bit for bit: fields, stop.
+
+LEX_NS = 3
+
+
+def _lex_formula(c, pE, pW, pN, pS, f, ee, ew, en, omega, h):
+    nc = ee + ew + en + 1.0
+    return c * (1.0 - omega) + (omega / nc) * ((ee * pE + ew * pW) + (en * pN + pS) - f * (h * h))
+
+
+def _lex_res(c, pE, pW, pN, pS, f, ee, ew, en, h):
+    return (1.0 / (h * h)) * (ee * (pE - c) + ew * (pW - c) + en * (pN - c) + (pS - c)) - f
+
+
+def lex_reference(f, nx, ny, omega, h, K, tol):
+    """The reference's loop (scalar Python, one domain): sweep j = 1..ny,
+    i = 1..nx in place, then the max-norm residual; stop when it is <= tol."""
+    p = np.zeros_like(f)
+    for k in range(1, K + 1):
+        for j in range(1, ny + 1):
+            for i in range(1, nx + 1):
+                ee, ew, en = float(i < nx), float(i > 1), float(j < ny)
+                p[j, i] = _lex_formula(p[j, i], p[j, i + 1], p[j, i - 1], p[j + 1, i], p[j - 1, i], f[j, i],
+                                       ee, ew, en, omega, h)
+        r = 0.0
+        for j in range(1, ny + 1):
+            for i in range(1, nx + 1):
+                ee, ew, en = float(i < nx), float(i > 1), float(j < ny)
+                r = max(r, abs(_lex_res(p[j, i], p[j, i + 1], p[j, i - 1], p[j + 1, i], p[j - 1, i], f[j, i],
+                                        ee, ew, en, h)))
+        if not r > tol:
+            return p, k
+    return p, K
+
+
+def _lex_skewed(rank, world, nx, ny, f_full, omega, h, K, tol, exchange, ormax):
+    """One rank's skewed solve of K iterations; returns its owned rows and the
+    iteration the (all-reduced) bits stop at (K: none)."""
+    j0, j1 = strip_rows(rank, world, ny)
+    lo = j0 - HALO
+    rows = np.arange(lo, j1 + HALO + 1)
+    valid = (rows >= 0) & (rows <= ny + 1)
+    f = np.zeros((len(rows), nx + 2)); f[valid] = f_full[rows[valid]]
+    jj, ii = np.meshgrid(rows, np.arange(nx + 2), indexing="ij")
+    s = ii + jj
+    inside = (ii >= 1) & (ii <= nx) & (jj >= 1) & (jj <= ny)
+    inside[0, :] = inside[-1, :] = False
+    owned = inside & (jj >= j0) & (jj <= j1)
+    ee, ew, en = (ii < nx).astype(float), (ii > 1).astype(float), (jj < ny).astype(float)
+    p = np.zeros_like(f)
+    exceed = np.zeros(K + 1, dtype=bool)
+    hlast = nx + ny + 2 * (K - 1) + 1  # (the last cell's residual is evaluated one half-sweep after its update)
+    for H0 in range(2, hlast + 1, 2 * LEX_NS):
+        exchange(p)
+        for hh in range(H0, H0 + 2 * LEX_NS):
+            before = p.copy()
+            pE, pW = np.roll(before, -1, 1), np.roll(before, 1, 1)
+            pN, pS = np.roll(before, -1, 0), np.roll(before, 1, 0)
+            upd = inside & ((s & 1) == (hh & 1)) & (s <= hh) & (hh <= s + 2 * (K - 1))
+            p = np.where(upd, _lex_formula(before, pE, pW, pN, pS, f, ee, ew, en, omega, h), before)
+            # residuals of the cells updated in half-sweep hh - 1 (iteration k)
+            k = (hh - 1 - s) // 2 + 1
+            ev = owned & ((s & 1) != (hh & 1)) & (k >= 1) & (k <= K) & (s <= hh - 1)
+            r = _lex_res(before, np.roll(p, -1, 1), pW, np.roll(p, -1, 0), pS, f, ee, ew, en, h)
+            hit = ev & (np.abs(r) > tol)
+            exceed[np.unique(k[hit])] = True
+    bits = ormax(exceed[1:].astype(np.float64))  # OR over the ranks
+    stop = next((k for k in range(1, K) if not bits[k - 1] > 0.0), K)
+    return j0, j1, p[HALO:-HALO].copy(), stop
+
+
+def _lex_worker(rank, world, port, q, nx, ny, K, tol):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    try:
+        def exchange(p):
+            if rank > 0:
+                dist.send(torch.from_numpy(p[HALO:2 * HALO].copy()), rank - 1)
+                buf = torch.empty((HALO, p.shape[1]), dtype=torch.float64); dist.recv(buf, rank - 1)
+                p[:HALO] = buf.numpy()
+            if rank < world - 1:
+                buf = torch.empty((HALO, p.shape[1]), dtype=torch.float64); dist.recv(buf, rank + 1)
+                dist.send(torch.from_numpy(p[-2 * HALO:-HALO].copy()), rank + 1)
+                p[-HALO:] = buf.numpy()
+
+        def ormax(a):
+            t = torch.from_numpy(a.copy())
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return t.numpy()
+
+        f_full = _lex_source(nx, ny)
+        h, omega = 1.0 / nx, 1.7
+        j0, j1, strip, stop = _lex_skewed(rank, world, nx, ny, f_full, omega, h, K, tol, exchange, ormax)
+        if stop < K:  # the stop is replayed: exactly `stop` iterations from the initial field
+            j0, j1, strip, _ = _lex_skewed(rank, world, nx, ny, f_full, omega, h, stop, -1.0, exchange, ormax)
+        q.put((rank, j0, j1, strip, stop))
+    finally:
+        dist.destroy_process_group()
+
+
+def _lex_source(nx, ny):
+    rng = np.random.default_rng(11)
+    f = np.zeros((ny + 2, nx + 2))
+    f[1:ny + 1, 1:nx + 1] = rng.standard_normal((ny, nx))
+    return f
+
+
+@pytest.mark.parametrize("mode", ["capped", "converging"])
+def test_two_rank_reference_order_equals_reference_loop(mode):
+    """Two gloo ranks of 20 rows, the skewed reference-order launches with the
+    halo exchange and the OR-ed exceedance bits (the GPU rank path of
+    ordering = lex, ABI 12) against the reference's own loop on one domain:
+    the same stop iteration, the same field bit for bit."""
+    world, nx, ny, K = 2, 18, 40, 24
+    h, omega = 1.0 / nx, 1.7
+    f = _lex_source(nx, ny)
+    if mode == "capped":
+        tol = 0.0
+    else:  # a tolerance met first at iteration 15
+        res = []
+        for k in range(1, K + 1):
+            pk, _ = lex_reference(f, nx, ny, omega, h, k, -1.0)
+            r = max(abs(_lex_res(pk[j, i], pk[j, i + 1], pk[j, i - 1], pk[j + 1, i], pk[j - 1, i], f[j, i],
+                                 float(i < nx), float(i > 1), float(j < ny), h))
+                    for j in range(1, ny + 1) for i in range(1, nx + 1))
+            res.append(r)
+        assert all(a > b for a, b in zip(res, res[1:]))
+        tol = 0.5 * (res[13] + res[14])
+    ref, kstop = lex_reference(f, nx, ny, omega, h, K, tol)
+    if mode == "converging":
+        assert kstop == 15
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_lex_worker, args=(r, world, port, q, nx, ny, K, tol)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    out = sorted(q.get(timeout=300) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for rank, j0, j1, strip, stop in out:
+        assert stop == kstop
+        assert np.array_equal(strip.view(np.int64), ref[j0:j1 + 1].view(np.int64)), rank

@@ -44,7 +44,7 @@ def test_nm_exports_match_header():
 
 
 def test_abi_version():
-    assert _lib.lib().cfd_abi_version() == 11
+    assert _lib.lib().cfd_abi_version() == 12
 
 
 def test_params_struct_layout_matches_header(tmp_path):
@@ -190,8 +190,9 @@ def test_sweeps_per_launch_validated_before_device(case, spl, kw, msg):
 def test_reference_order_is_the_default():
     """cfd_params_init selects the reference's own sweep order (bit-identical
     output) for the three reference cases; the Python classes take it on one
-    device and red-black on ranks, where the reference order is rejected
-    before any device is touched (DESIGN.md §5)."""
+    device and on ranks (ABI 12). A backwards step whose block is under 2 cells
+    wide runs the one-workgroup kernel, one strip only: on ranks it is rejected
+    before any device is touched."""
     for case in ("cavity", "channel", "backwards_step"):
         out = _lib.CfdParams()
         assert _lib.lib().cfd_params_init(C.params.CASE_IDS[case], 0, 0, 0, 0, ctypes.byref(out)) == 0
@@ -201,9 +202,11 @@ def test_reference_order_is_the_default():
     assert out.ordering == _lib.ORDER["rb"]  # (no reference solver: the rank path's order)
     cp = C.solver.to_cparams(C.make_params("cavity"))
     assert cp.ordering == _lib.ORDER["lex"]
-    h = _lib.lib().cfd_create_rank(ctypes.byref(cp), 0, 1, 63, None)
+    sp = C.solver.to_cparams(C.make_params("backwards_step"))
+    sp.step_i = 1
+    h = _lib.lib().cfd_create_rank(ctypes.byref(sp), 0, 1, sp.ny, None)
     assert not h
-    assert b"one device" in _lib.lib().cfd_last_error()
+    assert b"no ranks" in _lib.lib().cfd_last_error()
 
 
 @pytest.mark.parametrize("case,knob,value", [
@@ -299,8 +302,9 @@ def test_host_binaries_built_and_print_usage():
 def test_bench_traffic_provenance(tmp_path, monkeypatch):
     """bench.py reports roofline.traffic from the newest committed PMC pass of
     the same workload only when that pass profiled the kernel instance that
-    ran (its kernel_match), with the file and commit as traffic_source; a
-    mismatched kernel, grid or sweep count gives traffic null."""
+    ran (its kernel_match) from the same translation-unit sources (its
+    source_hash), with the file, commit and hash as traffic_source; a
+    mismatched kernel, grid, sweep count or source hash gives traffic null."""
     import json as _json
 
     import bench
@@ -312,8 +316,13 @@ def test_bench_traffic_provenance(tmp_path, monkeypatch):
     prof = tmp_path / "profiles"
     prof.mkdir()
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    from cfd_amd.provenance import source_hash, tu_sources
+
+    h = source_hash("poisson_multi_kernel<0, 4, true>")
+    assert h and len(h) == 64 and any(f.endswith("march.hpp") for f in tu_sources("solver"))
+    assert source_hash("poisson_tile_kernel<0, true>") != h  # (another translation unit)
     rec = {"kernel_match": "poisson_multi_kernel<0, 4, true>", "nx": 64, "rows": 66, "sweeps_per_launch": 4,
-           "hbm_bytes_per_launch": 123.0, "commit": "abc123"}
+           "hbm_bytes_per_launch": 123.0, "commit": "abc123", "source_hash": h}
     (prof / "r4_pmc_cavity_rb_64x64.json").write_text(_json.dumps(dict(rec, hbm_bytes_per_launch=99.0)))
     (prof / "r5_pmc_cavity_rb_64x64.json").write_text(_json.dumps(rec))
     t, src = bench.pmc_traffic("cavity", "rb", 64, 64, 66, 4, "poisson_multi_kernel<0, 4, true>")
@@ -324,3 +333,8 @@ def test_bench_traffic_provenance(tmp_path, monkeypatch):
     assert t is None and "mismatch" in src["reason"]
     t, src = bench.pmc_traffic("channel", "rb", 64, 64, 66, 4, "poisson_open_proof_kernel<1, 4>")
     assert t is None and "no profiles" in src["reason"]
+    # a profile taken on other kernel sources (stale) or without a hash: traffic null
+    for stale in ({"source_hash": "0" * 64}, {"source_hash": None}):
+        (prof / "r6_pmc_cavity_rb_64x64.json").write_text(_json.dumps(dict(rec, **stale)))
+        t, src = bench.pmc_traffic("cavity", "rb", 64, 64, 66, 4, "poisson_multi_kernel<0, 4, true>")
+        assert t is None and "stale" in src["reason"]
