@@ -48,7 +48,7 @@ ORDER = {"rb": 0, "lex": 1}
 SWITCH = {"auto": 0, "on": 1, "off": 2}  # enum cfd_switch
 TUNING = {"pair_wps": 0, "wave_wps": 1, "lexw_waves": 2, "lexw_edge_pct": 3, "pair_edge_pct": 4,
           "march_min_th": 5, "tent_th": 6, "lexw_ramp_pct": 7, "tile_rounds": 8, "march_order": 9,
-          "lexw_left": 10, "resident": 11}  # enum cfd_tuning
+          "lexw_left": 10, "resident": 11, "lexw_updown": 12}  # enum cfd_tuning
 SOR_KERNEL = {0: "none", 1: "march", 2: "tile", 3: "small", 4: "lexw", 5: "lex", 6: "smlex", 7: "resident"}  # enum cfd_sor_kernel
 
 

@@ -329,11 +329,12 @@ __device__ __forceinline__ double lx_res(const WaveCtx<CAVITY>& x, double eN, in
 // ramp tiles, for cells outside the grid or inactive at H-1). Straight-line
 // code: branches on the row-uniform conditions split the march loop and
 // serialise its loads, so they become scalar coefficients and thresholds.
-template <int ROT, int JPAR, int COLOR, int MODE, bool EDGE, bool STORE, bool RES>
+template <int ROT, int JPAR, int COLOR, int MODE, bool EDGE, bool STORE, bool RES, bool UP = false>
 __device__ __forceinline__ void lx_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LxCol (&cc)[2],
                                        double2 (&W)[5], int j, int X, const LxAct& act, const double2& fc, int& exi) {
   double2& m = W[LX_SLOT(X)];
-  const double2 nb = W[LX_SLOT(X + 1)], sb = W[LX_SLOT(X - 1)];  // rows j+1 (N), j-1 (S)
+  // rows j+1 (N), j-1 (S): ring position X+1 holds row j+1 marching down, j-1 marching up (lx_march UP)
+  const double2 nb = W[LX_SLOT(UP ? X - 1 : X + 1)], sb = W[LX_SLOT(UP ? X + 1 : X - 1)];
   const double2 old = m;
   const bool upd = j > x.rmin && j < x.rmax;  // row-uniform (rows 1..ny: rmin/rmax exclude the ghost rows)
   const bool top = j == x.g.ny;
@@ -355,7 +356,7 @@ __device__ __forceinline__ void lx_row(const WaveCtx<CAVITY>& x, const LexCtx& l
   // residual of the other colour's cell of this lane (iteration of half-sweep
   // H-1), tested against +inf outside the wave's output rows; RES = false:
   // a row the sampled launch does not evaluate (lx_sweeps)
-  if constexpr (!RES) return;
+  if constexpr (!RES || UP) return;
   const bool rrow = j >= x.y0 && j < x.y1 && j >= x.g.j0 && j <= x.g.j1;  // row-uniform
   const double thr = rrow ? lc.tol : __builtin_huge_val();
   const double eN = top ? 0.0 : 1.0;
@@ -659,16 +660,18 @@ struct LxCols {
   LxoCol oc;
 };
 
-template <int CASE, int S, int NS, int T, int ROT, int PAR, int MODE, bool EDGE, bool RC>
+template <int CASE, int S, int NS, int T, int ROT, int PAR, int MODE, bool EDGE, bool RC, bool UP = false>
 __device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L,
                                           const LxCols<CASE>& cl, LexRun<NS>& s, int R, const LxAct& act, int& exi) {
   if constexpr (S < NS) {
     // red at R+2S+1 (parity PAR^1) in half-sweep H0+2S; black at R+2S+2 (PAR) in H0+2S+1
+    // (UP: at R-2S-1, R-2S-2, the same parities)
+    constexpr int D = UP ? -1 : 1;
     if constexpr (CASE == CAVITY) {
-      lx_row<ROT, PAR ^ 1, 0, MODE, EDGE, false, lx_res_row<MODE, T, 2 * S + 1>()>(
-          x, lc, cl.cc, s.w[S], R + 2 * S + 1, 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi);
-      lx_row<ROT, PAR, 1, MODE, EDGE, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>()>(
-          x, lc, cl.cc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi);
+      lx_row<ROT, PAR ^ 1, 0, MODE, EDGE, false, lx_res_row<MODE, T, 2 * S + 1>(), UP>(
+          x, lc, cl.cc, s.w[S], R + D * (2 * S + 1), 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi);
+      lx_row<ROT, PAR, 1, MODE, EDGE, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>(), UP>(
+          x, lc, cl.cc, s.w[S], R + D * (2 * S + 2), 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi);
     } else {
       lxo_row<CASE, ROT, PAR ^ 1, 0, MODE, EDGE, RC, false, lx_res_row<MODE, T, 2 * S + 1>(), S == 0, false>(
           x, lc, L, cl.oc, s.w[S], R + 2 * S + 1, 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi, s.d);
@@ -678,20 +681,22 @@ __device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx
           x, lc, L, cl.oc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi, s.d, nxt);
     }
     if constexpr (S + 1 < NS) s.w[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
-    lx_sweeps<CASE, S + 1, NS, T, ROT, PAR, MODE, EDGE, RC>(x, lc, L, cl, s, R, act, exi);
+    lx_sweeps<CASE, S + 1, NS, T, ROT, PAR, MODE, EDGE, RC, UP>(x, lc, L, cl, s, R, act, exi);
   }
 }
 
-template <int CASE, int NS, int T, int ROT, int PAR, int MODE, bool EDGE, bool RC>  // PAR = parity of R, T = step of the unroll
+template <int CASE, int NS, int T, int ROT, int PAR, int MODE, bool EDGE, bool RC, bool UP = false>  // PAR = parity of R, T = step of the unroll
 __device__ __forceinline__ void lx_step(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L,
                                         const LxCols<CASE>& cl, LexRun<NS>& s, int R, unsigned long long bit) {
+  constexpr int D = UP ? -1 : 1;
   s.w[0][LX_SLOT(0)] = s.np[LX_SLOT(0)];
   s.fr[LX_S10(1)] = s.nf[LX_SLOT(0)];
-  s.np[LX_SLOT(-4)] = lx_ld(x, x.pin, R - 4);
-  s.nf[LX_SLOT(-4)] = lx_ld(x, x.f, R - 3);
+  s.np[LX_SLOT(-4)] = lx_ld(x, x.pin, R - 4 * D);
+  s.nf[LX_SLOT(-4)] = lx_ld(x, x.f, R - 3 * D);
   int exi = 0;
   const LxAct act = lx_act<MODE, CASE == BACKSTEP && EDGE && RC>(lc, x.gi, R);
-  lx_sweeps<CASE, 0, NS, T, ROT, PAR, MODE, EDGE, RC>(x, lc, L, cl, s, R, act, exi);
+  lx_sweeps<CASE, 0, NS, T, ROT, PAR, MODE, EDGE, RC, UP>(x, lc, L, cl, s, R, act, exi);
+  if constexpr (UP) return;  // (no residuals marching up)
   if constexpr ((MODE & LX_SAMPLE) && (T < 1 || T > 2 * NS)) return;  // (no residual row at this step)
   s.mask |= exi ? bit : 0ull;
 }
@@ -720,12 +725,22 @@ __device__ __forceinline__ void lexw_flush(const LexCtl& L, int sh, int q0, cons
   }
 }
 
-template <int CASE, int NS, int MODE, bool EDGE, bool RC = false>
+// UP (the cavity's steady interior bands, lexw_updown): the same march
+// mirrored - the front row climbs from below the band, sweep S red at R-2S-1,
+// black at R-2S-2 - without residuals (a residual needs its row's south
+// neighbour before and north neighbour after a half-sweep: marching up that
+// would hold rows for a step longer; the down bands' sampled rows prove the
+// iterations). Neighbouring bands marching in opposite directions read their
+// shared halo rows at the same time (both at the start or both at the end of
+// the launch): they come from L2 instead of HBM twice.
+template <int CASE, int NS, int MODE, bool EDGE, bool RC = false, bool UP = false>
 __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L, int y0, int y1,
                                          int c0, int lane, int shard) {
+  static_assert(!UP || (CASE == CAVITY && !(MODE & LX_ACT) && !EDGE), "upward march: the cavity's unmasked interior bands");
   constexpr int H = 2 * NS + 1;
-  const int Rb0 = y1 - 1 + H;
-  const int Rbeg = Rb0 + (Rb0 & 1);  // even first front row: compile-time colours
+  constexpr int D = UP ? -1 : 1;
+  const int Rb0 = UP ? y0 - H : y1 - 1 + H;
+  const int Rbeg = UP ? Rb0 - (Rb0 & 1) : Rb0 + (Rb0 & 1);  // even first front row: compile-time colours
   const int nsteps = (y1 - y0) + 2 * H + (Rb0 & 1);
   LexRun<NS> s;
   const double2 z = make_double2(0.0, 0.0);
@@ -739,8 +754,8 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
     constexpr int ROT = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      s.np[LX_SLOT(-q)] = lx_ld(x, x.pin, Rbeg - q);
-      s.nf[LX_SLOT(-q)] = lx_ld(x, x.f, Rbeg - (q - 1));
+      s.np[LX_SLOT(-q)] = lx_ld(x, x.pin, Rbeg - D * q);
+      s.nf[LX_SLOT(-q)] = lx_ld(x, x.f, Rbeg - D * (q - 1));
     }
   }
   s.mask = 0ull;
@@ -750,6 +765,21 @@ __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx&
   if constexpr (EDGE && CASE != CAVITY)
     cl.oc = LxoCol{lxo_kind(x, x.gi), lxo_kind(x, x.gi + 1), lxs_class(x, x.gi), lxs_class(x, x.gi + 1)};
   int R = Rbeg;
+  if constexpr (UP) {
+    for (int st = 0; st < nsteps; st += 10, R += 10) {
+      lx_step<CASE, NS, 0, 0, 0, MODE, EDGE, RC, true>(x, lc, L, cl, s, R, 0ull);
+      lx_step<CASE, NS, 1, 1, 1, MODE, EDGE, RC, true>(x, lc, L, cl, s, R + 1, 0ull);
+      lx_step<CASE, NS, 2, 2, 0, MODE, EDGE, RC, true>(x, lc, L, cl, s, R + 2, 0ull);
+      lx_step<CASE, NS, 3, 3, 1, MODE, EDGE, RC, true>(x, lc, L, cl, s, R + 3, 0ull);
+      lx_step<CASE, NS, 4, 4, 0, MODE, EDGE, RC, true>(x, lc, L, cl, s, R + 4, 0ull);
+      lx_step<CASE, NS, 5, 0, 1, MODE, EDGE, RC, true>(x, lc, L, cl, s, R + 5, 0ull);
+      lx_step<CASE, NS, 6, 1, 0, MODE, EDGE, RC, true>(x, lc, L, cl, s, R + 6, 0ull);
+      lx_step<CASE, NS, 7, 2, 1, MODE, EDGE, RC, true>(x, lc, L, cl, s, R + 7, 0ull);
+      lx_step<CASE, NS, 8, 3, 0, MODE, EDGE, RC, true>(x, lc, L, cl, s, R + 8, 0ull);
+      lx_step<CASE, NS, 9, 4, 1, MODE, EDGE, RC, true>(x, lc, L, cl, s, R + 9, 0ull);
+    }
+    return;
+  }
   // (nsteps + 9 <= 127 by the host's band limit: bits t/2 < 64)
 #define LX_BIT(T) ((((st + (T)) >> 1) < 64) ? (1ull << ((st + (T)) >> 1)) : 0ull)
   for (int st = 0; st < nsteps; st += 10, R -= 10) {
@@ -861,6 +891,9 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   const int blk = (bl < L8) ? (bl % 8) * (nblk / 8) + bl / 8 : bl;
   const int tile = blk * 4 + wv;
   int ctile, y0, y1;
+  // (flags bit 4: the cavity's odd bands march up where the tile is wholly
+  // active - steady launches, and the ramp launches' full interior tiles)
+  bool up = false;
   if (rp.nb > 0) {  // ramp launch (LexRamp): binary search of the tile's band
     int lo = 0, hi = rp.nb - 1;
     while (lo < hi) {
@@ -876,6 +909,7 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     int half;
     lexw_ramp_waves(rp, pl.ctiles, lo, ca, cb, tile - (int)(e >> 16), &ctile, &half);
     if (ctile > cb) return;
+    up = (lo & 1) && (flags & 16) && half < 0;
     int rlo, rhi;
     lexw_rows(g, H0, K, NS, ctile, &rlo, &rhi, OPEN);
     y0 = max(rp.row0 + lo * rp.th, rlo);
@@ -902,6 +936,7 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
         band = t / nci;
         // (the step's split bands: part 0 here, the others below)
         if (ctile - pl.xa < pl.xn && ctile >= pl.xa && band - pl.xb < pl.xbn && band >= pl.xb) part = 0;
+        up = (band & 1) && (flags & 16);
       } else {
         const int u = t - nci * nbi, nx = pl.xn * pl.xbn;
         if (u >= nx * (pl.xparts - 1)) return;
@@ -999,10 +1034,12 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
       // march, not the masked one - the masked wall marches set the ramps' time)
       if (edge && full && CFD_LEXW_RAMP_EDGE_FULL) { LX_PATH(0); lx_march<CASE, NS, SM, true>(x, lc, L, y0, y1, c0, lane, shard); }
       else if (edge) { LX_PATH(0); lx_march<CASE, NS, LX_ACT | SM, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (full && SAMPLE && up) { LX_PATH(1); lx_march<CASE, NS, SM, false, false, SAMPLE>(x, lc, L, y0, y1, c0, lane, shard); }
       else if (full) { LX_PATH(1); lx_march<CASE, NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard); }
       else { LX_PATH(2); lx_march<CASE, NS, LX_ACT | SM, false>(x, lc, L, y0, y1, c0, lane, shard); }
     } else {
       if (edge) { LX_PATH(0); lx_march<CASE, NS, SM, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (SAMPLE && up) { LX_PATH(3); lx_march<CASE, NS, SM, false, false, SAMPLE>(x, lc, L, y0, y1, c0, lane, shard); }
       else { LX_PATH(3); lx_march<CASE, NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard); }
     }
   } else {

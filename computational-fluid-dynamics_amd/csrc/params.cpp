@@ -176,6 +176,7 @@ extern "C" int cfd_tuning_default(const cfd_params* p, int knob, int* value) {
     case CFD_TUNE_TILE_ROUNDS: *value = cav ? 1 : 0; return CFD_OK;
     case CFD_TUNE_MARCH_ORDER: *value = 0; return CFD_OK;
     case CFD_TUNE_LEXW_LEFT: *value = 1; return CFD_OK;
+    case CFD_TUNE_LEXW_UPDOWN: *value = 1; return CFD_OK;
     case CFD_TUNE_RESIDENT:  // (the channel 4096x512: 4.96 vs lexw 10.3, red-black 5.03 vs march 8.15 us per sweep)
       *value = (cav || p->case_id == CFD_CHANNEL) ? 1 : 0;
       return CFD_OK;

@@ -259,6 +259,7 @@ class Solver {
       case CFD_TUNE_MARCH_ORDER: march_flags = (march_flags & ~8) | (v ? 8 : 0); break;
       case CFD_TUNE_LEXW_LEFT: lexw_left = v != 0; break;
       case CFD_TUNE_RESIDENT: res_knob = v != 0; break;
+      case CFD_TUNE_LEXW_UPDOWN: lexw_updown = v != 0; break;
       default: throw Error(CFD_E_ARG, "unknown tuning knob");
     }
   }
@@ -274,6 +275,7 @@ class Solver {
   int lexw_edge_pct = 100;  // wall-tile band length, % of the interior band (cfd_tuning_default: 75 up to 2048 rows)
   int lexw_ramp_pct = 0;    // ramp launches: bands at least this % of the steady plan's (CFD_TUNE_LEXW_RAMP_PCT)
   bool lexw_left = true;    // backwards step: the left column tiles' class (CFD_TUNE_LEXW_LEFT)
+  bool lexw_updown = true;  // cavity steady launches: odd interior bands march up (CFD_TUNE_LEXW_UPDOWN)
   // the multi-block reference-order march (lexw.hpp): cavity (1-4 sweeps per
   // launch), channel and backwards step (4; 3 on strips). The step's solid
   // rules need a block of at least 2 columns and 2 rows (si >= 2, jb <= ny-1);
@@ -396,7 +398,7 @@ class Solver {
       // for the cavity only
       for (int knob : {CFD_TUNE_LEXW_EDGE_PCT, CFD_TUNE_PAIR_EDGE_PCT, CFD_TUNE_MARCH_MIN_TH, CFD_TUNE_TENT_TH,
                        CFD_TUNE_LEXW_RAMP_PCT, CFD_TUNE_TILE_ROUNDS, CFD_TUNE_MARCH_ORDER, CFD_TUNE_LEXW_LEFT,
-                       CFD_TUNE_RESIDENT}) {
+                       CFD_TUNE_RESIDENT, CFD_TUNE_LEXW_UPDOWN}) {
         int v = 0;
         if (cfd_tuning_default(&P, knob, &v) == CFD_OK) set_tuning_value(knob, v);
       }
@@ -1112,7 +1114,7 @@ class Solver {
   void launch_lexw(int ns, bool steady, bool sample, const PairPlan& pl, const Geo& g, const double* pin,
                    double* pout, const double* f, const LexCtl& L, int H0, int K, int ka, int kb, bool replay,
                    int waves) {
-    const int fl = (replay ? 4 : 0) | (lexw_left_class() ? 8 : 0);
+    const int fl = (replay ? 4 : 0) | (lexw_left_class() ? 8 : 0) | (lexw_updown ? 16 : 0);
     const int ne = pl.ctiles >= 2 ? 2 : 1;
     int ntiles = ne * (pl.nbe0 + pl.nbe1) + (pl.ctiles - ne) * (pl.nb0 + pl.nb1);
     LexRamp rp{};

@@ -236,12 +236,15 @@ enum cfd_tuning {
   CFD_TUNE_LEXW_LEFT = 10,    /* reference-order backwards step: 1 = the column tiles left of the step's column end
                                  at the block's bottom row and march as a channel below it (default), 0 = the
                                  per-cell masked march over every row that reaches the block (ABI 10) */
-  CFD_TUNE_RESIDENT = 11      /* the cavity and the channel, one strip, no ranks, both orders (red-black: with the
+  CFD_TUNE_RESIDENT = 11,     /* the cavity and the channel, one strip, no ranks, both orders (red-black: with the
                                  proof-mode test; the reference order: sampled exceedance bits, an iteration they
                                  leave open finished by the multi-block march): 1 = the whole solve as one
                                  persistent register-resident launch where the grid fits one tile per CU and every
                                  tile can be resident at once (default: cavity 1024^2 2.2 us per sweep against the
                                  LDS tiles' 5.2), 0 = never (ABI 11) */
+  CFD_TUNE_LEXW_UPDOWN = 12   /* reference-order cavity, steady launches: 1 = every other interior band marches up
+                                 (no residuals there; neighbouring bands read their shared halo rows at the same
+                                 time), 0 = every band marches down (ABI 12) */
 };
 int cfd_set_tuning(cfd_solver* s, int knob, int value);
 /* The default a solver created from these parameters starts with (host only, no

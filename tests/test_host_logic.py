@@ -216,7 +216,7 @@ def test_reference_order_is_the_default():
     ("cavity", "tile_rounds", 1), ("channel", "tile_rounds", 0), ("rayleigh_benard", "tile_rounds", 1),
     ("cavity", "tent_th", 64), ("channel", "lexw_edge_pct", 75), ("backwards_step", "lexw_ramp_pct", 100), ("cavity", "lexw_ramp_pct", 0),
     ("cavity@4096", "lexw_edge_pct", 100), ("cavity@1024", "lexw_edge_pct", 75),
-    ("backwards_step", "lexw_left", 1), ("cavity", "lexw_left", 1), ("cavity/rb", "resident", 1), ("channel/rb", "resident", 1),
+    ("backwards_step", "lexw_left", 1), ("cavity", "lexw_left", 1), ("cavity", "lexw_updown", 1), ("cavity/rb", "resident", 1), ("channel/rb", "resident", 1),
     ("channel", "resident", 1), ("backwards_step", "resident", 0),
 ])
 def test_tuning_defaults(case, knob, value):
