@@ -854,7 +854,8 @@ __host__ __device__ inline void lexw_rows(const Geo& g, int H0, int K, int ns, i
 
 // diagnostic build only (CFD_LEXW_STAMPS=1, never the product library): per
 // launch (H0 / 2NS) and march path (0 wall tiles, 1 unmasked, 2 masked, 3
-// steady interior, 4 the step's block-crossing tiles on the masked march, 5
+// steady interior, 4 the step's block-crossing tiles on the masked march or
+// the cavity's steady interior bands marching up, 5
 // the step's left tiles, 6 / 7 row-checked open-case ramp / steady) the maximum and the
 // sum of the waves' march cycles and the wave count (solver.hip
 // cfd_lexw_stamps, scripts/dbg/lexw_stamps.py)
@@ -1039,7 +1040,7 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
       else { LX_PATH(2); lx_march<CASE, NS, LX_ACT | SM, false>(x, lc, L, y0, y1, c0, lane, shard); }
     } else {
       if (edge) { LX_PATH(0); lx_march<CASE, NS, SM, true>(x, lc, L, y0, y1, c0, lane, shard); }
-      else if (SAMPLE && up) { LX_PATH(3); lx_march<CASE, NS, SM, false, false, SAMPLE>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (SAMPLE && up) { LX_PATH(4); lx_march<CASE, NS, SM, false, false, SAMPLE>(x, lc, L, y0, y1, c0, lane, shard); }
       else { LX_PATH(3); lx_march<CASE, NS, SM, false>(x, lc, L, y0, y1, c0, lane, shard); }
     }
   } else {
