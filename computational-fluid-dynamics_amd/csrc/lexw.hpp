@@ -865,6 +865,13 @@ __host__ __device__ inline void lexw_rows(const Geo& g, int H0, int K, int ns, i
 #if CFD_LEXW_STAMPS
 constexpr int LEXW_STAMP_LAUNCHES = 8192;
 static __device__ unsigned long long lexw_stamp_buf[LEXW_STAMP_LAUNCHES * 8 * 3];
+// per wave of the launches li = LEXW_WSTAMP_L0 .. +LEXW_WSTAMP_N-1: {cycles, start
+// memtime, ctile << 32 | y0, xcc id}, by tile (is a slow wave slow in every launch?)
+#ifndef LEXW_WSTAMP_L0
+#define LEXW_WSTAMP_L0 1500
+#endif
+constexpr int LEXW_WSTAMP_N = 8, LEXW_WSTAMP_T = 4096;
+static __device__ unsigned long long lexw_wstamp_buf[LEXW_WSTAMP_N * LEXW_WSTAMP_T * 4];
 #endif
 
 // One launch of NS lexicographic-order sweeps (half-sweeps H0 .. H0+2NS-1) on
@@ -889,7 +896,10 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
   const int nblk = (int)gridDim.x;
   const int L8 = (nblk / 8) * 8;
   const int bl = (int)blockIdx.x;
-  const int blk = (bl < L8) ? (bl % 8) * (nblk / 8) + bl / 8 : bl;
+#ifndef CFD_LEXW_XCD_ROT
+#define CFD_LEXW_XCD_ROT 0  // (diagnostic A/B: rotate which XCD marches which range of tiles)
+#endif
+  const int blk = (bl < L8) ? ((bl + CFD_LEXW_XCD_ROT) % 8) * (nblk / 8) + bl / 8 : bl;
   const int tile = blk * 4 + wv;
   int ctile, y0, y1;
   // (flags bit 4: the cavity's odd bands march up where the tile is wholly
@@ -1093,6 +1103,16 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
       atomicMax(b, cyc);
       atomicAdd(b + 1, cyc);
       atomicAdd(b + 2, 1ull);
+      const int wl = li - LEXW_WSTAMP_L0;
+      if (wl >= 0 && wl < LEXW_WSTAMP_N && tile < LEXW_WSTAMP_T) {
+        unsigned long long* w = lexw_wstamp_buf + ((size_t)wl * LEXW_WSTAMP_T + tile) * 4;
+        unsigned xcc = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        w[0] = cyc;
+        w[1] = (unsigned long long)t0_;
+        w[2] = ((unsigned long long)(unsigned)ctile << 32) | (unsigned)y0;
+        w[3] = xcc;
+      }
     }
   }
 #endif

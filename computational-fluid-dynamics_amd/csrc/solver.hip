@@ -2353,6 +2353,12 @@ extern "C" int cfd_lexw_stamps(unsigned long long* out, int n) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(cfd::lexw_stamp_buf), (size_t)n * 8) == hipSuccess ? n : -1;
 }
+// per-wave records of a window of launches (lexw.hpp lexw_wstamp_buf)
+extern "C" int cfd_lexw_wstamps(unsigned long long* out, int n) {
+  if (n > cfd::LEXW_WSTAMP_N * cfd::LEXW_WSTAMP_T * 4) n = cfd::LEXW_WSTAMP_N * cfd::LEXW_WSTAMP_T * 4;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(cfd::lexw_wstamp_buf), (size_t)n * 8) == hipSuccess ? n : -1;
+}
 #endif
 
 #if CFD_MARCH_STAMPS
