@@ -48,4 +48,27 @@ out["wave_mean_quantiles"] = q.tolist()
 slow = m > np.quantile(m, 0.98)
 out["slowest_2pct"] = {"ctiles": np.unique(ct[slow]).tolist()[:40], "y0": np.unique(y0[slow]).tolist()[:40],
                        "xcc": np.bincount(xcc[slow], minlength=8).tolist()}
+# what-if: the waves of a band pair (down band 2q over up band 2q-1, same
+# column tile) share their rows at run time - each pair ends at 2 Td Tu / (Td + Tu)
+ys = sorted(np.unique(y0[(ct > 0) & (ct < ct.max())]))
+bidx = {y: k for k, y in enumerate(ys)}
+sim = []
+for l in range(N):
+    tmax = 0.0
+    byk = {}
+    for w in range(cyc.shape[1]):
+        if 0 < ct[w] < ct.max():
+            byk[(int(ct[w]), bidx[int(y0[w])])] = cyc[l, w]
+        else:
+            tmax = max(tmax, cyc[l, w])
+    for (c, b), t in byk.items():
+        if b == 0:
+            tmax = max(tmax, t)
+        elif b % 2 == 0:
+            tu = byk.get((c, b - 1))
+            tmax = max(tmax, t if tu is None else 2 * t * tu / (t + tu))
+        elif (c, b + 1) not in byk:
+            tmax = max(tmax, t)
+    sim.append(tmax)
+out["pair_share_launch_max"] = sim
 print(json.dumps(out, indent=1))
