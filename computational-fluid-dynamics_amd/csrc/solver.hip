@@ -1640,7 +1640,7 @@ class Solver {
     }
     if (res_on && P.ordering == CFD_ORDER_LEX) {
       T.sor_kernel = CFD_SOR_RESIDENT;
-      if (!solve_resident_lex(out)) solve_lexw(out);  // an iteration no sample settles: the exact path
+      solve_resident_lex_segments(out);  // (an iteration no sample settles: an exact window, then resident again)
       return;
     }
     if (use_lexw()) {
@@ -1660,13 +1660,169 @@ class Solver {
     }
     if (res_on) {
       T.sor_kernel = CFD_SOR_RESIDENT;
-      int k0 = 0;
-      if (solve_resident(out, k0)) return;
-      solve_rb(out, k0);  // an iteration the proof left open: exact launches from k0
+      solve_resident_segments(out);  // (an iteration the proof leaves open: an exact window, then resident again)
       return;
     }
     T.sor_kernel = tile_on ? CFD_SOR_TILE : CFD_SOR_MARCH;
     solve_rb(out, 0);
+  }
+
+  // A solve on the resident launch, in segments (round 6). A launch that
+  // leaves an iteration open hands the next stretch of the solve to the exact
+  // launches - a window of RES_WINDOW_LAUNCHES of them from the field reached
+  // (red-black: the launch's proven iterations replayed; the reference order:
+  // its intact input) - and, unless the reference stops inside the window or
+  // at its end, relaunches the resident kernel from the window's field for
+  // the rest of the solve. Each segment is a solve from the field it starts
+  // with: an SOR sweep depends on nothing but the current field (and the
+  // channel's ghosts as stored, which the last sweep's refresh left), and the
+  // reference's loop goes on through every iteration before the open one, so
+  // the segments' iterations are the reference's, bit for bit. A solve from
+  // rest (its first iterations' residuals live at the lid's corners: no proof,
+  // no sampled row) thus pays one window, not the whole solve on the exact
+  // path (round 5: ~2.3x a later step at 1024^2). After RES_MAX_SEGMENTS
+  // windows the exact path finishes the solve.
+  static constexpr int RES_WINDOW_LAUNCHES = 32, RES_MAX_SEGMENTS = 8;
+  struct CapGuard {  // the segment's iteration cap in P.max_iters (every solve path reads the cap there)
+    int& ref;
+    int saved;
+    CapGuard(int& r, int v) : ref(r), saved(r) { ref = v; }
+    ~CapGuard() { ref = saved; }
+  };
+  double tol_host() {
+    double t2[2];
+    HIPC(hipMemcpyAsync(t2, tolv, sizeof t2, hipMemcpyDeviceToHost, st));
+    HIPC(hipStreamSynchronize(st));
+    return t2[0];
+  }
+  int res_segments = 0;  // segments of the last solve (tests: a solve from rest relaunches the resident kernel)
+  void solve_resident_segments(cfd_step_info* out) {
+    const int K = P.max_iters;
+    int kdone = 0;
+    cfd_step_info si{0, 0.0};
+    res_segments = 0;
+    for (int seg = 0;; ++seg) {
+      ++res_segments;
+      int k0 = 0;
+      const long long to0 = T.resident_timeouts;
+      bool done;
+      {
+        CapGuard cg(P.max_iters, K - kdone);
+        done = solve_resident(&si, k0, seg == 0);
+      }
+      if (done) {
+        kdone += si.sor_iterations;
+        break;
+      }
+      const bool broken = T.resident_timeouts != to0;  // (not co-resident after all: no relaunch)
+      // the field after kdone + k0 iterations: the replay's output (k0 > 0) or the intact input
+      if (k0 > 0) pcur = (pcur + 1) % nbufs();
+      kdone += k0;
+      const bool last = broken || seg + 1 >= RES_MAX_SEGMENTS;
+      const int w = last ? K - kdone : std::min(RES_WINDOW_LAUNCHES * sweeps_per_launch(), K - kdone);
+      {
+        CapGuard cg(P.max_iters, w);
+        rb_fresh = false;
+        rb_exact = !last;
+        solve_rb(&si, 0);
+        rb_fresh = true;
+        rb_exact = false;
+      }
+      kdone += si.sor_iterations;
+      // the reference stopped inside the window, the cap, or iteration kdone's
+      // exact residual (the window's last, which its launches do not test) meets
+      // the tolerance: the solve ends here
+      if (last || si.sor_iterations < w || kdone >= K || !(si.residual > tol_host())) break;
+    }
+    if (out) {
+      out->sor_iterations = kdone;
+      out->residual = si.residual;
+    }
+  }
+  // the reference order: the resident launch's open iteration leaves its
+  // input intact; the exact window is the multi-block march from that field
+  // (lexw.hpp, every cell's residual evaluated: kexact 1), its stop replayed
+  // from the window's initial field (kept in B_P2)
+  void solve_resident_lex_segments(cfd_step_info* out) {
+    const int K = P.max_iters;
+    int kdone = 0;
+    cfd_step_info si{0, 0.0};
+    double res = 0.0;
+    res_segments = 0;
+    for (int seg = 0;; ++seg) {
+      ++res_segments;
+      const long long to0 = T.resident_timeouts;
+      bool done;
+      {
+        CapGuard cg(P.max_iters, K - kdone);
+        done = solve_resident_lex(&si, seg == 0);
+      }
+      if (done) {
+        kdone += si.sor_iterations;
+        res = si.residual;
+        break;
+      }
+      if (seg == 0 && T.resident_timeouts != to0) {  // (not co-resident: the exact path takes the whole solve)
+        solve_lexw(out);
+        return;
+      }
+      const bool last = T.resident_timeouts != to0 || seg + 1 >= RES_MAX_SEGMENTS;
+      // (the window reaches past the open iteration: its launches cost the
+      // skew's ramps, ~(nx + ny) / 2NS of them, whatever its length)
+      const int ko = std::max(1, si.sor_iterations);
+      const int w = last ? K - kdone : std::min(std::max(RES_WINDOW_LAUNCHES * 2 * lexw_ns(), ko + 64), K - kdone);
+      int k2 = 0;
+      const bool stopped = lexw_window(w, &k2, &res);
+      kdone += k2;
+      if (stopped || last || kdone >= K) break;
+    }
+    lex_hint = 0;  // (the segments keep no sampled-row hint)
+    if (out) {
+      out->sor_iterations = kdone;
+      out->residual = res;
+    }
+  }
+  // w reference-order iterations from the field in pbuf(pcur & 1) with every
+  // cell's residual evaluated; returns true when the reference stops inside
+  // the window or at its end (the exact residual of its last iteration), with
+  // *k = the iterations run (the field in pbuf(pcur)) and *res that residual
+  bool lexw_window(int w, int* k, double* res) {
+    const int ns = lexw_ns();
+    const int b0 = pcur & 1;
+    for (auto& s : S)
+      HIPC(hipMemcpyAsync(s.b[B_P2], s.b[pbuf(b0)], (size_t)s.g.nrows * pitch * sizeof(double),
+                          hipMemcpyDeviceToDevice, st));
+    lex_set_both(B_P2);
+    const size_t words = (size_t)LEXW_SHARDS * ((lexw_offset() + w + (P.nx + P.ny) / 2 + 256) / 64 + 2);
+    if (lexbits_words < words) {
+      if (lexbits) HIPC(hipFree(lexbits));
+      lexbits = nullptr;
+      HIPC(hipMalloc(&lexbits, words * sizeof(unsigned long long)));
+      lexbits_words = words;
+    }
+    lex_reset_tests();
+    HIPC(hipEventRecord(ev_a, st));
+    int k2 = -1, code = 0;
+    const int n = run_lexw(b0, w, true, 1, 1, &k2, &code, false);
+    T.poisson_launches += n;
+    T.poisson_sweeps += (long long)n * ns;
+    int fin = (b0 + n) % 2, iters = w;
+    if (code == 1) {  // the reference stops at k2 < w: redo k2 iterations from the window's field
+      iters = k2;
+      lex_set_both(B_P2);
+      fin = lex_replay(b0, k2);
+    }
+    HIPC(hipEventRecord(ev_b, st));
+    *res = final_residual(pbuf(fin));
+    float ms = 0.f;
+    HIPC(hipEventElapsedTime(&ms, ev_a, ev_b));
+    T.poisson_ms += ms;
+    long long owned = 0;
+    for (auto& s : S) owned += (long long)(s.g.j1 - s.g.j0 + 1) * P.nx;
+    T.poisson_cell_updates += owned * iters;
+    pcur = fin;
+    *k = iters;
+    return code == 1 || !(*res > tol_host());
   }
 
   // The register-resident solve (resident.hpp): one persistent launch runs the
@@ -1674,15 +1830,16 @@ class Solver {
   // iteration k0 + 1's group was left open by the proof, the field after k0
   // iterations is in the output buffer of "launch 0" (pbuf(base + 1)), and
   // solve_rb goes on from there with exact residuals (k0 = 0: from scratch).
-  bool solve_resident(cfd_step_info* out, int& k0) {
+  bool solve_resident(cfd_step_info* out, int& k0, bool fresh = true) {
     Strip& s = S[0];
     const int base = pcur;
     const size_t fbytes = (size_t)s.g.nrows * pitch * sizeof(double);
     double* pin = s.b[pbuf(base)];
     double* pout = s.b[pbuf((base + 1) % nbufs())];
     // the cavity starts each solve from a zero field (cavity-01.cpp:610-611),
-    // the channel from the previous pressure (channel-01.cpp:636)
-    if (P.case_id == CFD_CAVITY) HIPC(hipMemsetAsync(pin, 0, fbytes, st));
+    // the channel from the previous pressure (channel-01.cpp:636); a later
+    // segment of the solve (solve_resident_segments) from the field reached
+    if (P.case_id == CFD_CAVITY && fresh) HIPC(hipMemsetAsync(pin, 0, fbytes, st));
     const bool open = P.case_id == CFD_CHANNEL;
     const int cid = open ? CHANNEL : CAVITY;
     solve_tolerance();
@@ -1779,7 +1936,7 @@ class Solver {
   // sampled residuals. Returns false (nothing changed but the tolerance) when
   // an iteration before the cap has no sampled exceedance: it may be the
   // reference's stop, which only the exact evaluation settles (solve_lexw).
-  bool solve_resident_lex(cfd_step_info* out) {
+  bool solve_resident_lex(cfd_step_info* out, bool fresh = true) {
     Strip& s = S[0];
     const int base = pcur & 1;
     const size_t fbytes = (size_t)s.g.nrows * pitch * sizeof(double);
@@ -1787,8 +1944,8 @@ class Solver {
     double* pout = s.b[pbuf(base ^ 1)];
     // the cavity starts each solve from a zero field (cavity-01.cpp:610-611);
     // the channel from the previous pressure (channel-01.cpp:636), left intact in
-    // p_in for the exact path
-    if (P.case_id == CFD_CAVITY) HIPC(hipMemsetAsync(pin, 0, fbytes, st));
+    // p_in for the exact path; a later segment from the field reached
+    if (P.case_id == CFD_CAVITY && fresh) HIPC(hipMemsetAsync(pin, 0, fbytes, st));
     solve_tolerance();
     if (!res_x[0])
       for (auto*& x : res_x) {
@@ -1843,6 +2000,7 @@ class Solver {
     }
     if (code == 2) {
       ++T.proof_fallbacks;
+      if (out) out->sor_iterations = h_stat[1];  // (the open iteration)
       return false;
     }
     if (code != 0 && code != 1) throw Error(CFD_E_STATE, "resident SOR solve: bad status");
@@ -1870,11 +2028,13 @@ class Solver {
   // iterations 1 .. k0 are done (solve_resident) and every one of them was
   // proven to go on; their field is launch 0's output, and the solve goes on
   // from there with one chunk of exact launches first.
+  bool rb_fresh = true;     // solve_rb starts a solve (the cavity's zero field); false: a segment from the field in pcur
+  bool rb_exact = false;    // solve_rb: exact residuals in every launch (the window after a resident launch's open iteration)
   void solve_rb(cfd_step_info* out, int k0) {
     const int base = pcur;
     HIPC(hipMemsetAsync(ring, 0, (size_t)RING * RES_SHARDS * SHARD_STRIDE * sizeof(double), st));
     HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
-    if (P.case_id == CFD_CAVITY && k0 == 0) {
+    if (P.case_id == CFD_CAVITY && k0 == 0 && rb_fresh) {
       // cavity-01.cpp:610-611: each solve starts from a zero field
       for (auto& s : S)
         HIPC(hipMemsetAsync(s.b[pbuf(base)], 0, (size_t)s.g.nrows * pitch * sizeof(double), st));
@@ -1899,7 +2059,7 @@ class Solver {
     // exact launches for one chunk, then proof mode again; windows over the
     // launches before it are empty (every one of their iterations was proven
     // to go on). Each launch record says which kind of value its slots hold.
-    int proof_from = proof_ok() ? 0 : INT32_MAX;  // first launch (index) in proof mode
+    int proof_from = (proof_ok() && !rb_exact) ? 0 : INT32_MAX;  // first launch (index) in proof mode
     int exact_from = 0;  // first launch whose iterations later launches test
     int iters = 0;
     if (k0 > 0) {  // "launch 0" = the resident solve's iterations 1 .. k0 (all proven to go on)

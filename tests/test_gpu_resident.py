@@ -466,3 +466,57 @@ def test_resident_check_every_equals_per_launch_paths(case, order):
     if order == "rb":
         assert all(k % 3 == 0 or k == cp.max_iters for k, _ in h1)
     assert_bits(p1, p2, f"{case} {order} check_every 3 p")
+
+
+# ---- a solve from rest returns to the resident launch (round 6) ----
+
+@pytest.mark.parametrize("order", ["rb", "lex"])
+def test_resident_step_from_rest_returns_to_resident(order):
+    """BASELINE configs[1] (1024^2, cap 10000) from rest: the first solve's
+    first iterations have residuals only at the lid's corners (no proof, no
+    sampled row), so the resident launch leaves an iteration open; an exact
+    window of launches settles that stretch and the resident kernel takes the
+    rest of the solve again (Solver::solve_resident_segments) - a handful of
+    launches, not the ~2500 exact ones of round 5 - and both steps stay bit
+    for bit the per-launch path's (LDS tiles / lexw). The first step's time
+    is printed beside the second's."""
+    cp = C.make_params("cavity", nx=1024, ny=1024)
+    g = C.CavitySolver(cp, ordering=order, device=0, small_solve="off", tuning={"resident": 1})
+    g.applyBoundaryConditions()
+    hist = [g.step()]
+    t1 = g.timing()
+    g.reset_timing()
+    hist.append(g.step())
+    t2 = g.timing()
+    fr = {n: g.field(n).copy() for n in FIELDS}
+    g.close()
+    tuning = {"resident": 0, "tile_rounds": 1}
+    w = C.CavitySolver(cp, ordering=order, device=0, small_solve="off", tuning=tuning)
+    w.applyBoundaryConditions()
+    hw = [w.step() for _ in range(2)]
+    fw = {n: w.field(n).copy() for n in FIELDS}
+    w.close()
+    assert hist == hw and hist[0][0] == cp.max_iters
+    for n in FIELDS:
+        assert_bits(fr[n], fw[n], f"{order} from rest {n}")
+    assert _lib.SOR_KERNEL[t1.sor_kernel] == "resident"
+    assert t1.proof_fallbacks >= 1  # (the open iteration at the start)
+    # (red-black: one exact window of 32 launches; the reference order's window
+    # pays the skew's ramps, ~(nx + ny) / 8 launches)
+    assert t1.poisson_launches <= (80 if order == "rb" else 400), t1.poisson_launches
+    assert t2.poisson_launches == 1
+    print(f"\n{order}: step 1 {t1.poisson_ms:.2f} ms in {t1.poisson_launches} launches, step 2 {t2.poisson_ms:.2f} ms"
+          f" ({t1.poisson_ms / t2.poisson_ms:.2f}x)")
+
+
+def test_resident_timeout_fallback_plan_is_co_resident():
+    """The plan only takes the persistent launch when the occupancy query
+    admits every tile at once (res_coresident_tiles): no resident solve of
+    the suite timed out."""
+    cp = C.make_params("cavity", nx=1024, ny=1024, max_iters=40)
+    g = C.CavitySolver(cp, ordering="lex", device=0, small_solve="off", tuning={"resident": 1})
+    g.applyBoundaryConditions()
+    g.step()
+    tm = g.timing()
+    g.close()
+    assert _lib.SOR_KERNEL[tm.sor_kernel] == "resident" and tm.resident_timeouts == 0
