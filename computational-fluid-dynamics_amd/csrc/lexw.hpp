@@ -456,16 +456,17 @@ __device__ __forceinline__ double lxo_value(const WaveCtx<CAVITY>& x, int rk, in
 }
 
 template <int CASE, int ROT, int JPAR, int COLOR, int MODE, bool EDGE, bool RC, bool STORE, bool RES, bool FIRSTH,
-          bool LASTH>
+          bool LASTH, bool UP = false>
 __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L, const LxoCol& cc,
                                         double2 (&W)[5], int j, int X, const LxAct& act, const double2& fc, int& exi,
                                         LxDefer& d, double2* nxt = nullptr) {
   // the step's general tiles (block boundary, ghosts): per-cell solid rules
   constexpr bool STEP = CASE == BACKSTEP && EDGE && RC;
+  static_assert(!UP || (!EDGE && !RC), "upward march: the open cases' unchecked interior bands");
   constexpr bool FULL = !(MODE & LX_SAMPLE);
   double2& m = W[LX_SLOT(X)];
-  double2& mn = W[LX_SLOT(X + 1)];
-  const double2 nb = mn, sb = W[LX_SLOT(X - 1)];  // rows j+1 (N), j-1 (S)
+  double2& mn = W[LX_SLOT(UP ? X - 1 : X + 1)];
+  const double2 nb = mn, sb = W[LX_SLOT(UP ? X + 1 : X - 1)];  // rows j+1 (N), j-1 (S)
   const double2 old = m;
   // row kind (row-uniform): 0 interior, 1 bottom ghost, 2 top ghost (or the
   // step's bottom solid row in a left tile: LexCtx::jg), 3 keep (halo edge /
@@ -578,7 +579,7 @@ __device__ __forceinline__ void lxo_row(const WaveCtx<CAVITY>& x, const LexCtx& 
     d2v mv = {m.x, m.y};
     __builtin_nontemporal_store(mv, reinterpret_cast<d2v*>(dst));
   }
-  if constexpr (!RES) return;
+  if constexpr (!RES || UP) return;
   const bool rrow = j >= x.y0 && j < x.y1 && j >= x.g.j0 && j <= lc.jr1;  // row-uniform
   const double thr = rrow ? lc.tol : __builtin_huge_val();
   const bool row1 = RC && j == 1;  // S is the bottom ghost: the cell's own value stands in
@@ -673,12 +674,12 @@ __device__ __forceinline__ void lx_sweeps(const WaveCtx<CAVITY>& x, const LexCtx
       lx_row<ROT, PAR, 1, MODE, EDGE, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>(), UP>(
           x, lc, cl.cc, s.w[S], R + D * (2 * S + 2), 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi);
     } else {
-      lxo_row<CASE, ROT, PAR ^ 1, 0, MODE, EDGE, RC, false, lx_res_row<MODE, T, 2 * S + 1>(), S == 0, false>(
-          x, lc, L, cl.oc, s.w[S], R + 2 * S + 1, 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi, s.d);
+      lxo_row<CASE, ROT, PAR ^ 1, 0, MODE, EDGE, RC, false, lx_res_row<MODE, T, 2 * S + 1>(), S == 0, false, UP>(
+          x, lc, L, cl.oc, s.w[S], R + D * (2 * S + 1), 2 * S + 1, act, s.fr[LX_S10(2 * S + 1)], exi, s.d);
       double2* nxt = nullptr;  // row R+2S+3 in the next sweep's ring (the step's corner write)
-      if constexpr (S + 1 < NS) nxt = &s.w[S + 1][LX_SLOT(2 * S + 3)];
-      lxo_row<CASE, ROT, PAR, 1, MODE, EDGE, RC, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>(), false, S == NS - 1>(
-          x, lc, L, cl.oc, s.w[S], R + 2 * S + 2, 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi, s.d, nxt);
+      if constexpr (S + 1 < NS && !UP) nxt = &s.w[S + 1][LX_SLOT(2 * S + 3)];
+      lxo_row<CASE, ROT, PAR, 1, MODE, EDGE, RC, S == NS - 1, lx_res_row<MODE, T, 2 * S + 2>(), false, S == NS - 1, UP>(
+          x, lc, L, cl.oc, s.w[S], R + D * (2 * S + 2), 2 * S + 2, act, s.fr[LX_S10(2 * S + 2)], exi, s.d, nxt);
     }
     if constexpr (S + 1 < NS) s.w[S + 1][LX_SLOT(2 * S + 2)] = s.w[S][LX_SLOT(2 * S + 2)];
     lx_sweeps<CASE, S + 1, NS, T, ROT, PAR, MODE, EDGE, RC, UP>(x, lc, L, cl, s, R, act, exi);
@@ -736,7 +737,7 @@ __device__ __forceinline__ void lexw_flush(const LexCtl& L, int sh, int q0, cons
 template <int CASE, int NS, int MODE, bool EDGE, bool RC = false, bool UP = false>
 __device__ __forceinline__ void lx_march(const WaveCtx<CAVITY>& x, const LexCtx& lc, const LexCtl& L, int y0, int y1,
                                          int c0, int lane, int shard) {
-  static_assert(!UP || (CASE == CAVITY && !(MODE & LX_ACT) && !EDGE), "upward march: the cavity's unmasked interior bands");
+  static_assert(!UP || (!(MODE & LX_ACT) && !EDGE && !RC), "upward march: the unmasked, unchecked interior bands");
   constexpr int H = 2 * NS + 1;
   constexpr int D = UP ? -1 : 1;
   const int Rb0 = UP ? y0 - H : y1 - 1 + H;
@@ -1078,6 +1079,7 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
         LX_PATH(0);
         lx_march<CASE, NS, SM, true, true>(x, lc, L, y0, y1, c0, lane, shard);
       } else if (edge) { LX_PATH(0); lx_march<CASE, NS, LX_ACT | SM, true, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (full && SAMPLE && up) { LX_PATH(1); lx_march<CASE, NS, SM, false, false, SAMPLE>(x, lc, L, y0, y1, c0, lane, shard); }
       else if (full) { LX_PATH(1); lx_march<CASE, NS, SM, false, false>(x, lc, L, y0, y1, c0, lane, shard); }
       else if (rc && efull && CFD_LEXW_RAMP_EDGE_FULL) {  // (row-checked bands likewise: the steady rc march)
         LX_PATH(6);
@@ -1087,6 +1089,7 @@ __global__ __launch_bounds__(256, RAMP ? 2 : CFD_LEXW_MIN_WAVES(NS)) void poisso
     } else {
       if (edge) { LX_PATH(0); lx_march<CASE, NS, SM, true, true>(x, lc, L, y0, y1, c0, lane, shard); }
       else if (rc) { LX_PATH(7); lx_march<CASE, NS, SM, false, true>(x, lc, L, y0, y1, c0, lane, shard); }
+      else if (SAMPLE && up) { LX_PATH(3); lx_march<CASE, NS, SM, false, false, SAMPLE>(x, lc, L, y0, y1, c0, lane, shard); }
       else { LX_PATH(3); lx_march<CASE, NS, SM, false, false>(x, lc, L, y0, y1, c0, lane, shard); }
     }
   }

@@ -242,7 +242,7 @@ enum cfd_tuning {
                                  persistent register-resident launch where the grid fits one tile per CU and every
                                  tile can be resident at once (default: cavity 1024^2 2.2 us per sweep against the
                                  LDS tiles' 5.2), 0 = never (ABI 11) */
-  CFD_TUNE_LEXW_UPDOWN = 12   /* reference-order cavity, steady launches: 1 = every other interior band marches up
+  CFD_TUNE_LEXW_UPDOWN = 12   /* reference order, wholly active interior tiles: 1 = every other band marches up
                                  (no residuals there; neighbouring bands read their shared halo rows at the same
                                  time), 0 = every band marches down (ABI 12) */
 };
