@@ -459,3 +459,64 @@ def test_two_rank_reference_order_equals_reference_loop(mode):
     for rank, j0, j1, strip, stop in out:
         assert stop == kstop
         assert np.array_equal(strip.view(np.int64), ref[j0:j1 + 1].view(np.int64)), rank
+
+
+# ---- the reference order's sequential sums on ranks (Solver::seq_sum_ranks) ----
+
+def _chain_worker(rank, world, port, q, nx, ny):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    try:
+        f = _lex_source(nx, ny)
+        j0, j1 = strip_rows(rank, world, ny)
+        acc = torch.zeros(1, dtype=torch.float64)
+        for r in range(world):  # one round per link, every rank in every round (the loopback transport's rule)
+            if r == rank:
+                s = float(acc[0]) if rank > 0 else 0.0
+                for j in range(j0, j1 + 1):  # the reference's loop order, one rounding per term
+                    for i in range(1, nx + 1):
+                        s += float(f[j, i])
+                acc[0] = s
+            if r + 1 < world:
+                if rank == r:
+                    dist.send(acc, r + 1)
+                elif rank == r + 1:
+                    dist.recv(acc, r)
+        if rank == world - 1:  # the last rank's total back to every rank
+            for p in range(world - 1):
+                dist.send(acc, p)
+        else:
+            dist.recv(acc, world - 1)
+        q.put((rank, float(acc[0])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rank_chained_sequential_sum_equals_one_loop(world):
+    """The open cases' source sum (channel-01.cpp:620-628) on ranks in the
+    reference's order: rank r continues rank r-1's running sum, the last
+    rank's total goes back to all - bit for bit the single loop's sum (a
+    per-rank partial sum all-reduced would re-associate it)."""
+    nx, ny = 37, 48
+    f = _lex_source(nx, ny)
+    one = 0.0
+    for j in range(1, ny + 1):
+        for i in range(1, nx + 1):
+            one += float(f[j, i])
+    partial = sum(sum(float(f[j, i]) for j in range(a, b + 1) for i in range(1, nx + 1))
+                  for a, b in (strip_rows(r, world, ny) for r in range(world)))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_chain_worker, args=(r, world, port, q, nx, ny)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    out = sorted(q.get(timeout=120) for _ in range(world))
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for _, v in out:
+        assert v.hex() == one.hex()
+    assert partial != one or world == 1  # (re-associated partial sums differ in the last bits here)
