@@ -92,7 +92,7 @@ def test_switches_default_to_auto_and_map():
     assert (lp.proof_test, lp.small_solve, lp.overlap) == (0, 0, 0)
     cp = C.solver.to_cparams(C.make_params("cavity"), proof_test="off", small_solve="on", overlap="off")
     assert (cp.proof_test, cp.small_solve, cp.overlap) == (2, 1, 2)
-    assert set(_lib.TUNING.values()) == set(range(12))
+    assert set(_lib.TUNING.values()) == set(range(13))
 
 
 @pytest.mark.parametrize("case", ["cavity", "channel", "backwards_step"])
