@@ -67,7 +67,8 @@ class Timing(ctypes.Structure):
                 ("poisson_overlapped", ctypes.c_longlong), ("poisson_steady_ms", ctypes.c_double),
                 ("poisson_steady_launches", ctypes.c_longlong),
                 ("proof_fallbacks", ctypes.c_longlong), ("sor_kernel", ctypes.c_int),
-                ("resident_timeouts", ctypes.c_longlong)]
+                ("resident_timeouts", ctypes.c_longlong), ("seqsum_chunks", ctypes.c_longlong),
+                ("seqsum_serial_chunks", ctypes.c_longlong)]
 
 
 # every symbol include/cfd_amd.h declares: name -> (restype, argtypes)

@@ -123,6 +123,9 @@ class Solver {
   double *ring = nullptr, *srcmax = nullptr, *divmax = nullptr, *tolv = nullptr, *partials = nullptr,
          *total = nullptr;
   int* stop = nullptr;
+  void* seqws = nullptr;  // seq_sum_launch's chunk records (seqsum.hip)
+  size_t seqws_bytes = 0;
+  int* seqcnt = nullptr;  // chunks the sequential sums ran as the plain chain (device counter)
   size_t npart = 0;
   int* h_stat = nullptr;    // pinned: 2 x {stop, iter}
   double* h_shard = nullptr;  // pinned: RES_SHARDS*SHARD_STRIDE
@@ -321,11 +324,23 @@ class Solver {
   // total goes back to every rank: the same bits as one device. Every rank
   // issues the same group sequence (the loopback transport needs it; RCCL
   // takes the empty groups as no-ops).
+  void seq_sum(const Strip& s, const double* a, const double* b, int mode, double* acc, bool accumulate) {
+    T.seqsum_chunks += seq_sum_launch(s.g, C, a, b, mode, acc, accumulate ? 1 : 0, seqws, seqws_bytes, seqcnt, st);
+    check_launch("seq_sum");
+  }
+  // the device counter of plain-chain chunks into T (and back to zero)
+  void flush_seq_count() {
+    int n = 0;
+    HIPC(hipMemcpyAsync(&n, seqcnt, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPC(hipMemsetAsync(seqcnt, 0, sizeof(int), st));
+    HIPC(hipStreamSynchronize(st));
+    T.seqsum_serial_chunks += n;
+  }
   void seq_sum_ranks(int a, int b, int mode, double* acc) {
     const int R = comm->nranks, me = comm->rank;
     const Strip& s = S[0];
     for (int q = 0; q < R; ++q) {
-      if (q == me) seq_sum_launch(s.g, C, s.b[a], b >= 0 ? s.b[b] : nullptr, mode, acc, me > 0, st);
+      if (q == me) seq_sum(s, s.b[a], b >= 0 ? s.b[b] : nullptr, mode, acc, me > 0);
       if (q + 1 < R) {
         comm_group_start(comm);
         if (me == q) comm_send(comm, acc, 1, q + 1, st);
@@ -459,6 +474,12 @@ class Solver {
     HIPC(hipMalloc(&stop, 2 * sizeof(int)));
     HIPC(hipMalloc(&resmax, RES_SHARDS * SHARD_STRIDE * sizeof(double)));
     HIPC(hipMalloc(&cscr, 4 * sizeof(double)));
+    long long terms = 1;
+    for (auto& s : S) terms = std::max(terms, (long long)(std::min(s.g.j1, P.ny) - std::max(s.g.j0, 1) + 1) * P.nx);
+    seqws_bytes = seq_sum_workspace(terms);
+    HIPC(hipMalloc(&seqws, seqws_bytes));
+    HIPC(hipMalloc(&seqcnt, 8 * sizeof(int)));  // [0] the count ([1..5]: CFD_SEQ_STAMPS builds' phase ticks)
+    HIPC(hipMemsetAsync(seqcnt, 0, 8 * sizeof(int), st));
     HIPC(hipMemsetAsync(ring, 0, ringn * sizeof(double), st));
     HIPC(hipMemsetAsync(tolv, 0, 4 * sizeof(double), st));
     HIPC(hipMemsetAsync(stop, 0, 2 * sizeof(int), st));
@@ -551,6 +572,10 @@ class Solver {
     for (double* p : {ring, srcmax, divmax, tolv, total, partials, resmax, cscr})
       if (p) (void)hipFree(p);
     ring = srcmax = divmax = tolv = total = partials = resmax = cscr = nullptr;
+    if (seqws) (void)hipFree(seqws);
+    if (seqcnt) (void)hipFree(seqcnt);
+    seqws = nullptr;
+    seqcnt = nullptr;
     if (lexbits) (void)hipFree(lexbits);
     lexbits = nullptr;
     if (lexflags) (void)hipFree(lexflags);
@@ -731,7 +756,7 @@ class Solver {
         seq_sum_ranks(B_F, -1, 0, total);
       } else if (P.ordering == CFD_ORDER_LEX) {  // the reference's sequential sum, bit for bit (strips in order)
         for (size_t q = 0; q < S.size(); ++q)
-          seq_sum_launch(S[q].g, C, S[q].b[B_F], nullptr, 0, total, q > 0, st);
+          seq_sum(S[q], S[q].b[B_F], nullptr, 0, total, q > 0);
       } else {
         sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total);
       }
@@ -2281,7 +2306,7 @@ class Solver {
       seq_sum_ranks(B_UC, B_VC, 1, total + 1);
     else if (P.ordering == CFD_ORDER_LEX)
       for (size_t q = 0; q < S.size(); ++q)
-        seq_sum_launch(S[q].g, C, S[q].b[B_UC], S[q].b[B_VC], 1, total + 1, q > 0, st);
+        seq_sum(S[q], S[q].b[B_UC], S[q].b[B_VC], 1, total + 1, q > 0);
     else
       sum_partials_kernel<<<1, 256, 0, st>>>(partials, (int)npart, total + 1);
     check_launch("sum_partials");
@@ -2521,6 +2546,17 @@ extern "C" int cfd_lexw_wstamps(unsigned long long* out, int n) {
 }
 #endif
 
+#ifdef CFD_SEQ_STAMPS
+// diagnostic build only: seq_walk_kernel's phase ticks (100 MHz) since the last
+// call {batch loads, run records, single records, staging, plain chains}
+extern "C" int cfd_seq_stamps(cfd_solver* s, int* out) {
+  Solver* v = s->impl;
+  if (hipStreamSynchronize(v->st) != hipSuccess) return -1;
+  if (hipMemcpy(out, v->seqcnt + 1, 5 * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return hipMemset(v->seqcnt + 1, 0, 5 * sizeof(int)) == hipSuccess ? 5 : -1;
+}
+#endif
+
 #if CFD_MARCH_STAMPS
 // diagnostic build only: per wave {tile, column tile, band, y0, y1, interior
 // columns, safe, cycles} of the last poisson_multi_kernel launch
@@ -2565,6 +2601,7 @@ int cfd_get_timing(cfd_solver* s, cfd_timing* out) {
     if (!out) throw Error(CFD_E_ARG, "null output");
     Solver* v = S_(s);
     v->flush_step_time();
+    v->flush_seq_count();
     *out = v->T;
   });
 }
@@ -2572,6 +2609,7 @@ int cfd_reset_timing(cfd_solver* s) {
   return guard([&] {
     Solver* v = S_(s);
     v->flush_step_time();
+    v->flush_seq_count();
     v->T = cfd_timing{};
   });
 }

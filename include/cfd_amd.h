@@ -20,7 +20,7 @@
 extern "C" {
 #endif
 
-#define CFD_AMD_ABI_VERSION 12
+#define CFD_AMD_ABI_VERSION 13
 
 /* CFD_RAYLEIGH_BENARD (BASELINE configs[4]) has no solver in the reference
  * tree (only figures): it is the cavity's projection step with a resting lid
@@ -128,6 +128,10 @@ typedef struct cfd_timing {
   int sor_kernel;             /* enum cfd_sor_kernel: the SOR kernel family of the last solve (ABI 8) */
   long long resident_timeouts; /* resident whole-solve launches whose tiles' waits timed out (never expected:
                                   the plan checks co-residency); the exact launches took those solves (ABI 12) */
+  long long seqsum_chunks;        /* reference order: chunks of SQ_CH terms the sequential sums (source mean,
+                                     kinetic energy) were cut into (ABI 13) */
+  long long seqsum_serial_chunks; /* of those, the chunks that ran as the plain chain of adds (the first terms
+                                     from zero, binade crossings, ties); the rest were exact integer sums (ABI 13) */
 } cfd_timing;
 
 /* Which SOR kernel family ran a solve (cfd_timing.sor_kernel); every one gives the same bits for

@@ -44,7 +44,7 @@ def test_nm_exports_match_header():
 
 
 def test_abi_version():
-    assert _lib.lib().cfd_abi_version() == 12
+    assert _lib.lib().cfd_abi_version() == 13
 
 
 def test_params_struct_layout_matches_header(tmp_path):
