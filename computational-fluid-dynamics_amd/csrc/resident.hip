@@ -370,13 +370,14 @@ __device__ __forceinline__ bool res_spin_expired(unsigned long long t0) {
 // diagnostic build only (CFD_RES_STAMPS=1, never the product library): each
 // wave sums the shader-clock cycles of its group phases over the solve - 0
 // neighbour wait, 1 halo loads, 2 first exchange + proofs, 3 sweeps, 4 group
-// end (bands, drain, flag) - and counts its groups (5); read back by
-// cfd_res_stamps ([tile][wave][6], scripts/dbg/res_stamps.py)
+// end to the drained stores (bands, proofs / bits), 5 the barrier and the
+// flag - and counts its groups (6); read back by cfd_res_stamps
+// ([tile][wave][7], scripts/dbg/res_stamps.py)
 #ifndef CFD_RES_STAMPS
 #define CFD_RES_STAMPS 0
 #endif
 #if CFD_RES_STAMPS
-constexpr int RES_STAMP_SEGS = 6;
+constexpr int RES_STAMP_SEGS = 7;
 __device__ unsigned long long res_stamp_buf[256 * RES_MAXW * RES_STAMP_SEGS];
 #define RES_STAMP(seg)                                                          \
   do {                                                                          \
@@ -827,11 +828,12 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       dec = 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the bands (and wave 0's proofs / bits) drained before the flag
+    RES_STAMP(4);
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(myflag, (unsigned)(gi + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    RES_STAMP(4);
+    RES_STAMP(5);
 #if CFD_RES_STAMPS
-    st_acc[5] += 1;
+    st_acc[6] += 1;
 #endif
     if (dec == 1) {  // (every tile decides this at the same group)
       gfail = gdec;

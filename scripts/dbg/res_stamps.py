@@ -30,13 +30,14 @@ s.step()
 s.synchronize()
 tm = s.timing()
 L = _lib.lib()
-n = 256 * 8 * 6
+SEG = 7
+n = 256 * 8 * SEG
 buf = (ctypes.c_ulonglong * n)()
 L.cfd_res_stamps(buf, n)
-a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8, 6).astype(np.float64)
-groups = a[:, :, 5]
+a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8, SEG).astype(np.float64)
+groups = a[:, :, SEG - 1]
 used = groups > 0
-names = ["wait", "halo", "first_exchange", "sweeps", "end"]
+names = ["wait", "halo", "first_exchange", "sweeps", "drain", "barrier_flag"]
 out = {"case": case, "order": order, "nx": nx, "ny": ny, "iters": iters, "solve_ms": tm.poisson_ms, "launches": tm.poisson_launches,
        "fallbacks": tm.proof_fallbacks, "waves": int(used.sum()),
        "us_per_sweep": 1000 * tm.poisson_ms / iters}
@@ -51,11 +52,11 @@ for k, nm in enumerate(names):
 ctiles = (nx + 2 + 111) // 112
 tiles = np.arange(256)
 edge = ((tiles % ctiles) == 0) | ((tiles % ctiles) == ctiles - 1)
-for nm, k in (("sweeps", 3), ("wait", 0), ("end", 4)):
+for nm, k in (("sweeps", 3), ("wait", 0), ("drain", 4), ("barrier_flag", 5)):
     for cls, sel in (("edge_tiles", edge), ("inner_tiles", ~edge)):
         u = used & sel[:, None]
         if u.any():
             out[f"{nm}_{cls}_mean"] = round(float((a[:, :, k][u] / groups[u]).mean()), 1)
-tot = sum(a[:, :, k] for k in range(5))[used] / groups[used]
+tot = sum(a[:, :, k] for k in range(SEG - 1))[used] / groups[used]
 out["total_cyc_per_group_mean"] = round(float(tot.mean()), 1)
 print(json.dumps(out, indent=1))
