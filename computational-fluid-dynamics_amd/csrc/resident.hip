@@ -399,7 +399,7 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
                                                                              double* __restrict__ pout,
                                                                              const double* __restrict__ f, ResCtl R,
                                                                              ResPlan rp, int flags) {
-  constexpr int NS = RES_NS, H = RES_HALO, TW = RES_TW;
+  constexpr int NS = res_ns(LEX), H = res_halo(LEX), TW = res_tw(LEX);
   __shared__ double2 E[2][RES_MAXW][2][64];  // the waves' first / last rows after each half-sweep (by parity)
   __shared__ double red[2][RES_MAXW][NS + 1];  // red-black: per wave max |p' - p| per sweep, max |p| of the
                                                // input (group parity: wave 0 reads one while the waves write the other)
@@ -715,7 +715,9 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
       } else if constexpr (OPEN && !LEX) {
         // (MASK here: the short last group, as a loop in the general variant -
         // its conditional sweeps, unrolled, need ~160 more registers at 14 rows)
-        double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+        double dv[NS];
+#pragma unroll
+        for (int t = 0; t < NS; ++t) dv[t] = 0.0;
         bool ex = false;
 #pragma unroll 1
         for (int s = 0; s < nsw; ++s) {
@@ -724,16 +726,11 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
           exchange();
           res_half<CASE, RPW, 1, true, true, false, LEX>(c, L, p, fh, fl, Sx, Nx, fzm, tpm, dm, false, lh, ex);
           if (s + 1 < nsw) exchange();
-          d0 = s == 0 ? dm : d0;
-          d1 = s == 1 ? dm : d1;
-          d2 = s == 2 ? dm : d2;
-          d3 = s == 3 ? dm : d3;
+#pragma unroll
+          for (int t = 0; t < NS; ++t) dv[t] = s == t ? dm : dv[t];
         }
-        static_assert(NS == 4, "the loop's per-sweep proof values");
-        dmx[0] = d0;
-        dmx[1] = d1;
-        dmx[2] = d2;
-        dmx[3] = d3;
+#pragma unroll
+        for (int t = 0; t < NS; ++t) dmx[t] = dv[t];
         return;
       }
 #pragma unroll
@@ -956,22 +953,26 @@ void res_refresh(const Geo& g, double* p, hipStream_t st) {
   res_refresh_kernel<<<(n + 255) / 256, 256, 0, st>>>(g, p);
 }
 
-ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open) {
+ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open, bool lex) {
+  const int TW = res_tw(lex), HALO = res_halo(lex);
   ResPlan rp{};
   rp.lo = lo;
   rp.hi = hi;
   if ((lo & 1) != 0 || hi <= lo) return ResPlan{};
-  rp.ctiles = (nx + 2 + RES_TW - 1) / RES_TW;
+  rp.ctiles = (nx + 2 + TW - 1) / TW;
   const int rows = hi - lo;
   if (rp.ctiles > max_tiles) return ResPlan{};
   const int rt = std::max(1, max_tiles / rp.ctiles);
   rp.th = (rows + rt - 1) / rt;
-  rp.th = std::max(RES_HALO, (rp.th + 1) / 2 * 2);  // even (region row parity), at least one halo deep
+  rp.th = std::max(HALO, (rp.th + 1) / 2 * 2);  // even (region row parity), at least one halo deep
   rp.rtiles = (rows + rp.th - 1) / rp.th;
-  const int rr = rp.th + 2 * RES_HALO;
+  const int rr = rp.th + 2 * HALO;
   // 8 rows per wave; the channel also RES_RPW_OPEN (its source in LDS leaves
   // room: 4096x512's 102-row regions)
-  rp.rpw = rr <= 8 * RES_MAXW ? 8 : (open && rr <= RES_RPW_OPEN * RES_MAXW) ? RES_RPW_OPEN : 0;
+  rp.rpw = rr <= 8 * RES_MAXW ? 8
+           : (lex && !open && rr <= 10 * RES_MAXW) ? 10  // (the reference order's deeper groups: taller regions)
+           : (open && rr <= RES_RPW_OPEN * RES_MAXW) ? RES_RPW_OPEN
+                                                     : 0;
   if (rp.rpw == 0) return ResPlan{};  // a tile's region exceeds the register budget
   rp.waves = (rr + rp.rpw - 1) / rp.rpw;
   return rp;
@@ -986,6 +987,7 @@ ResKernel res_kernel(int case_id, bool lex, int rpw, size_t* lds) {
   *lds = 0;
   if (case_id == CAVITY && rpw == 8)
     return lex ? poisson_resident_kernel<CAVITY, 8, true> : poisson_resident_kernel<CAVITY, 8, false>;
+  if (case_id == CAVITY && rpw == 10 && lex) return poisson_resident_kernel<CAVITY, 10, true>;
   if (case_id == CHANNEL && rpw == 8) {
     *lds = res_flds_bytes<8>();
     return lex ? poisson_resident_kernel<CHANNEL, 8, true> : poisson_resident_kernel<CHANNEL, 8, false>;

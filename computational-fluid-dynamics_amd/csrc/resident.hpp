@@ -12,22 +12,26 @@
 // through HBM between sweeps except the tiles' edge bands.
 //
 // Layout: one workgroup of up to 8 waves per tile (at most one per CU, all
-// co-resident). A tile owns RES_TW = 112 columns x th rows (ghost rows /
-// columns included at the grid's edges) and holds a region of 128 columns x
-// (th + 2 RES_HALO) rows: lane l of every wave holds the column pair
+// co-resident). A tile owns res_tw = 112 (red-black) / 104 (reference order)
+// columns x th rows (ghost rows / columns included at the grid's edges) and
+// holds a region of 128 columns x (th + 2 res_halo) rows: lane l of every wave holds the column pair
 // (c0 + 2l, c0 + 2l + 1), wave w the region rows w*RPW .. w*RPW + RPW - 1 of p
-// in registers; the source as f*h^2 in registers (cavity, 8-row waves) or as
-// f in LDS (channel: 14-row waves fit 4096x512's 102-row regions). A
+// in registers; the source as f*h^2 in registers (cavity, 8- or 10-row waves)
+// or as f in LDS (channel: 14-row waves fit 4096x512's 102- / 110-row regions). A
 // half-sweep updates one colour in place (its neighbours are the other
 // colour): row neighbours within a lane's rows, column neighbours by DPP, the
 // rows of the neighbouring waves through LDS (one barrier per half-sweep). The
 // channel's ghost refreshes are cells of their own colour with copy rules.
 //
-// Groups: every RES_NS sweeps the tiles exchange their RES_HALO-deep edge
+// Groups: every res_ns sweeps the tiles exchange their res_halo-deep edge
 // bands through global memory (write-through stores, one flag per tile and
 // group; each tile waits for its <= 8 neighbours only): within a group the
 // halo goes stale by one cell per half-sweep and never reaches the owned
-// cells (RES_HALO = 2 RES_NS), exactly as the fused march launches' halos.
+// cells (res_halo = 2 res_ns), exactly as the fused march launches' halos.
+// Red-black groups are 4 sweeps (its proof bounds grow 9x per sweep of a
+// group), the reference order's 6: the hand-off (~3 us a hop, the
+// write-through stores' visibility) is paid every 6 sweeps instead of 4 for
+// 1.2x the redundant halo work (1024^2: 2.53 -> 2.11 us per sweep).
 //
 // Stop rule, with no grid barrier (completion spreads one tile per group, so
 // at group m every tile has finished group m - DIAM):
@@ -49,18 +53,23 @@
 
 namespace cfd {
 
-constexpr int RES_NS = 4;                    // sweeps per group
-constexpr int RES_HALO = 2 * RES_NS;         // halo cells per side (one per half-sweep)
-constexpr int RES_TW = 128 - 2 * RES_HALO;   // owned columns per tile (112)
+#ifndef CFD_RES_NS_LEX
+#define CFD_RES_NS_LEX 6
+#endif
+constexpr int RES_NS_RB = 4;                 // sweeps per group, red-black
+constexpr int RES_NS_LEX = CFD_RES_NS_LEX;   // sweeps per group, the reference's order
+__host__ __device__ constexpr int res_ns(bool lex) { return lex ? RES_NS_LEX : RES_NS_RB; }
+__host__ __device__ constexpr int res_halo(bool lex) { return 2 * res_ns(lex); }  // halo cells per side
+__host__ __device__ constexpr int res_tw(bool lex) { return 128 - 2 * res_halo(lex); }  // owned columns per tile
 constexpr int RES_MAXW = 8;                  // waves per workgroup, at most (2 per SIMD: 256 VGPRs each)
 constexpr int RES_LAG = 2;                   // group g is checked at the start of group g + RES_LAG
 constexpr int RES_REPLAY = 1;                // flags: no stop test (the host replays to a known count)
 
 struct ResPlan {
-  int ctiles, rtiles;  // column tiles (RES_TW owned columns) x row tiles (th owned rows)
+  int ctiles, rtiles;  // column tiles (res_tw owned columns) x row tiles (th owned rows)
   int th;              // owned rows per tile (even)
   int lo, hi;          // owned rows [lo, hi) of the strip (ghost rows included; lo even)
-  int waves;           // waves per workgroup (region rows th + 2 RES_HALO, rpw per wave)
+  int waves;           // waves per workgroup (region rows th + 2 res_halo, rpw per wave)
   int rpw;             // region rows per wave (template parameter of the kernel)
 };
 
@@ -84,11 +93,11 @@ struct ResCtl {
 
 // Tiling of a strip's owned rows [lo, hi) into at most max_tiles tiles, or
 // ctiles = 0 if the grid does not fit (the solver keeps the per-launch kernels)
-ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open = false);
+ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open, bool lex);
 // the channel's ghost refresh of a final field (red-black resident solve)
 void res_refresh(const Geo& g, double* p, hipStream_t st);
 constexpr int RES_RPW_OPEN = 14;  // rows per wave of the channel's larger tiles (reference order)
-__host__ __device__ inline int res_groups(int K) { return (K + RES_NS - 1) / RES_NS; }
+__host__ __device__ inline int res_groups(int K) { return (K + RES_NS_RB - 1) / RES_NS_RB; }  // (red-black)
 // unsigned words of flags + proofs + status, rounded to 16 B
 inline size_t res_state_words(int tiles, int K) {
   const size_t n = (size_t)tiles + (size_t)K + 1 + 8;

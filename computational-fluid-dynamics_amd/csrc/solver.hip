@@ -194,7 +194,7 @@ class Solver {
     if (P.case_id != CFD_CAVITY && !open) return;
     if (P.ordering == CFD_ORDER_RB && (!proof_enabled || !(C.proof_k > 0.0))) return;
     const Geo& g = S[0].g;
-    rplan = res_plan(P.nx, g.wj0, g.wj1 + 1, n_cu, open);
+    rplan = res_plan(P.nx, g.wj0, g.wj1 + 1, n_cu, open, P.ordering == CFD_ORDER_LEX);
     res_on = rplan.ctiles > 0 &&
              rplan.ctiles * rplan.rtiles <= res_coresident_tiles(open ? CHANNEL : CAVITY, P.ordering == CFD_ORDER_LEX,
                                                                  rplan, n_cu);

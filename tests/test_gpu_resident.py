@@ -23,7 +23,7 @@ from cfd_amd import _lib  # noqa: E402
 from test_gpu_parity import assert_bits, ofield  # noqa: E402
 
 FIELDS = ("p", "u", "v")
-RES_TW = 112  # owned columns per tile (resident.hpp)
+RES_TW = {"rb": 112, "lex": 104}  # owned columns per tile (resident.hpp res_tw)
 
 
 def run(cp, steps, resident=True, **kw):
@@ -174,11 +174,14 @@ def run_lex(cp, steps, resident=True, **kw):
 @pytest.mark.parametrize("nx,ny,steps,cap", [
     (300, 200, 3, 600), (333, 257, 3, 401), (1024, 64, 3, 600), (113, 130, 3, 500), (110, 110, 3, 300),
     (222, 96, 3, 403), (500, 300, 3, 1001), (100, 400, 3, 700),
+    (102, 80, 3, 500), (206, 90, 3, 403), (207, 60, 3, 300), (1024, 1100, 2, 300),
 ])
 def test_resident_lex_equals_lexw(nx, ny, steps, cap):
     """Capped solves in the reference's order: the resident launch (ramps
-    masked, residuals sampled) against the multi-launch march lexw.hpp, which
-    is bit-exact vs the reference loop (tests/test_gpu_lexw.py)."""
+    masked, residuals sampled; 6-sweep groups of 104-column tiles: nx + 2 =
+    104, 208, 209 on tile edges; 1024x1100: 68-row regions of 10-row waves)
+    against the multi-launch march lexw.hpp, which is bit-exact vs the
+    reference loop (tests/test_gpu_lexw.py)."""
     cp = params(nx, ny, max_iters=cap)
     hr, fr, tr = run_lex(cp, steps)
     hw, fw, tw = run_lex(cp, steps, resident=False)
@@ -258,7 +261,8 @@ def channel_solve(cp, f, p0, resident=True):
 
 
 @pytest.mark.parametrize("nx,ny,K", [(93, 31, 37), (300, 130, 25), (257, 64, 113), (224, 40, 17), (225, 41, 18),
-                                     (110, 120, 60), (222, 300, 41), (500, 200, 301), (1000, 60, 200)])
+                                     (110, 120, 60), (222, 300, 41), (500, 200, 301), (1000, 60, 200),
+                                     (102, 50, 33), (206, 70, 41), (207, 45, 19), (208, 66, 23)])
 def test_resident_channel_lex_vs_reference_order_oracle(nx, ny, K):
     """Capped channel solves from an arbitrary pressure (ghosts and corners
     included: the first sweep reads the ghosts as stored; the corners are never
