@@ -399,7 +399,7 @@ __global__ __launch_bounds__(RES_MAXW * 64, 1) void poisson_resident_kernel(Geo 
                                                                              double* __restrict__ pout,
                                                                              const double* __restrict__ f, ResCtl R,
                                                                              ResPlan rp, int flags) {
-  constexpr int NS = res_ns(LEX), H = res_halo(LEX), TW = res_tw(LEX);
+  constexpr int NS = res_ns(CASE != CAVITY, LEX), H = res_halo(CASE != CAVITY, LEX), TW = res_tw(CASE != CAVITY, LEX);
   __shared__ double2 E[2][RES_MAXW][2][64];  // the waves' first / last rows after each half-sweep (by parity)
   __shared__ double red[2][RES_MAXW][NS + 1];  // red-black: per wave max |p' - p| per sweep, max |p| of the
                                                // input (group parity: wave 0 reads one while the waves write the other)
@@ -954,7 +954,7 @@ void res_refresh(const Geo& g, double* p, hipStream_t st) {
 }
 
 ResPlan res_plan(int nx, int lo, int hi, int max_tiles, bool open, bool lex) {
-  const int TW = res_tw(lex), HALO = res_halo(lex);
+  const int TW = res_tw(open, lex), HALO = res_halo(open, lex);
   ResPlan rp{};
   rp.lo = lo;
   rp.hi = hi;

@@ -12,8 +12,8 @@
 // through HBM between sweeps except the tiles' edge bands.
 //
 // Layout: one workgroup of up to 8 waves per tile (at most one per CU, all
-// co-resident). A tile owns res_tw = 112 (red-black) / 104 (reference order)
-// columns x th rows (ghost rows / columns included at the grid's edges) and
+// co-resident). A tile owns res_tw = 112 (red-black) / 96 (reference order,
+// cavity) / 104 (reference order, channel) columns x th rows (ghost rows / columns included at the grid's edges) and
 // holds a region of 128 columns x (th + 2 res_halo) rows: lane l of every wave holds the column pair
 // (c0 + 2l, c0 + 2l + 1), wave w the region rows w*RPW .. w*RPW + RPW - 1 of p
 // in registers; the source as f*h^2 in registers (cavity, 8- or 10-row waves)
@@ -29,9 +29,11 @@
 // halo goes stale by one cell per half-sweep and never reaches the owned
 // cells (res_halo = 2 res_ns), exactly as the fused march launches' halos.
 // Red-black groups are 4 sweeps (its proof bounds grow 9x per sweep of a
-// group), the reference order's 6: the hand-off (~3 us a hop, the
-// write-through stores' visibility) is paid every 6 sweeps instead of 4 for
-// 1.2x the redundant halo work (1024^2: 2.53 -> 2.11 us per sweep).
+// group), the reference order's 8 (cavity) / 6 (channel: deeper halos would
+// not fit its regions in the waves' registers and LDS): the hand-off (~3 us
+// a hop, the write-through stores' visibility) is paid every 8 / 6 sweeps
+// instead of 4 for 1.2-1.4x the redundant halo work (1024^2: 2.53 -> 2.03 us
+// per sweep).
 //
 // Stop rule, with no grid barrier (completion spreads one tile per group, so
 // at group m every tile has finished group m - DIAM):
@@ -56,11 +58,17 @@ namespace cfd {
 #ifndef CFD_RES_NS_LEX
 #define CFD_RES_NS_LEX 6
 #endif
-constexpr int RES_NS_RB = 4;                 // sweeps per group, red-black
-constexpr int RES_NS_LEX = CFD_RES_NS_LEX;   // sweeps per group, the reference's order
-__host__ __device__ constexpr int res_ns(bool lex) { return lex ? RES_NS_LEX : RES_NS_RB; }
-__host__ __device__ constexpr int res_halo(bool lex) { return 2 * res_ns(lex); }  // halo cells per side
-__host__ __device__ constexpr int res_tw(bool lex) { return 128 - 2 * res_halo(lex); }  // owned columns per tile
+#ifndef CFD_RES_NS_LEX_CAV
+#define CFD_RES_NS_LEX_CAV 8
+#endif
+constexpr int RES_NS_RB = 4;                      // sweeps per group, red-black
+constexpr int RES_NS_LEX = CFD_RES_NS_LEX;        // sweeps per group, the reference's order (channel)
+constexpr int RES_NS_LEX_CAV = CFD_RES_NS_LEX_CAV;  // ... (cavity)
+__host__ __device__ constexpr int res_ns(bool open, bool lex) {
+  return lex ? (open ? RES_NS_LEX : RES_NS_LEX_CAV) : RES_NS_RB;
+}
+__host__ __device__ constexpr int res_halo(bool open, bool lex) { return 2 * res_ns(open, lex); }  // halo cells per side
+__host__ __device__ constexpr int res_tw(bool open, bool lex) { return 128 - 2 * res_halo(open, lex); }  // owned columns
 constexpr int RES_MAXW = 8;                  // waves per workgroup, at most (2 per SIMD: 256 VGPRs each)
 constexpr int RES_LAG = 2;                   // group g is checked at the start of group g + RES_LAG
 constexpr int RES_REPLAY = 1;                // flags: no stop test (the host replays to a known count)
