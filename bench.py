@@ -555,11 +555,13 @@ def run(args, rank: int, world: int, local_rank: int, comm, group, loopback: boo
                 "avg_launch_us": round(avg_launch_ms * 1e3, 2), "sweeps_per_launch": round(sweeps_per_launch, 4),
                 "us_per_sweep": round(avg_launch_ms * 1e3 / max(sweeps_per_launch, 1), 4),
                 # what bounds it (phase stamps of the cavity at 1024^2,
-                # profiles/r5/resident/): per 4-sweep group ~8.7 K cycles of sweeps
-                # against ~12 K of hand-off (band stores drained, neighbour flags,
-                # halo loads) - the VALU fraction above is not the limit
-                "note": "hand-off-latency bound: per 4-sweep group ~8.7 K cycles of sweeps vs ~12 K of edge-band "
-                        "hand-off (DESIGN.md section 4)",
+                # profiles/r5/resident/, profiles/r6/resident_granules/): per
+                # group ~8 K cycles of sweeps per 4 sweeps against ~12-14 K of
+                # hand-off (the write-through bands' visibility to the neighbour
+                # CUs, ~3 us) - the VALU fraction above is not the limit; the
+                # reference order's groups run 8 (cavity) / 6 (channel) sweeps
+                "note": "hand-off-latency bound: ~8 K cycles of sweeps per 4 sweeps vs ~12-14 K per edge-band hand-off "
+                        "(a group: red-black 4 sweeps, reference order 8 cavity / 6 channel; DESIGN.md section 4)",
             }
         if loopback:
             line["config"]["loopback_ranks_on_one_gpu"] = world
